@@ -1,0 +1,287 @@
+// gsr_api.hip -- C ABI of libgsr (declared in include/gsr.h).
+//
+// Host-side orchestration of the forward/backward kernel pipelines: argument validation with the
+// reference's error behaviour, workspace carving, the single num_rendered read-back per forward,
+// per-phase HIP-event timing, and a thread-local error string.  Mirrors the reference's
+// rasterize_points.cu glue + CudaRasterizer::Rasterizer::{forward,backward}.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gsr.h"
+#include "gsr_common.h"
+#include "gsr_internal.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e__ = (expr);                                                               \
+        if (e__ != hipSuccess) return fail(GSR_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e__)); \
+    } while (0)
+
+// ---- per-phase event profiling ----
+struct ProfRec { std::string phase; hipEvent_t a, b; };
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof;
+std::vector<hipEvent_t> g_evpool;
+
+hipEvent_t ev_get() {
+    if (!g_evpool.empty()) { hipEvent_t e = g_evpool.back(); g_evpool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+struct Phase {
+    hipStream_t s; const char *name; hipEvent_t a = nullptr, b = nullptr;
+    Phase(hipStream_t s_, const char *n) : s(s_), name(n) {
+        if (!g_prof_on) return;
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        a = ev_get(); b = ev_get();
+        if (a) (void)hipEventRecord(a, s);
+    }
+    ~Phase() {
+        if (!a || !b) return;
+        (void)hipEventRecord(b, s);
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof.push_back({name, a, b});
+    }
+};
+
+// pinned host word for the num_rendered read-back (one per thread)
+uint32_t *pinned_word() {
+    thread_local uint32_t *p = nullptr;
+    if (!p && hipHostMalloc((void **)&p, sizeof(uint32_t) * 4, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    return p;
+}
+
+int check_common(const gsr_camera *cam, const gsr_gaussians *g, bool need_opacity) {
+    if (!cam || !g) return fail(GSR_ERR_ARG, "null camera or gaussians");
+    if (g->P < 0) return fail(GSR_ERR_ARG, "P must be >= 0");
+    if (cam->image_width <= 0 || cam->image_height <= 0)
+        return fail(GSR_ERR_ARG, "image size must be positive (got %dx%d)", cam->image_width, cam->image_height);
+    const int gx = div_up(cam->image_width, kTileW), gy = div_up(cam->image_height, kTileH);
+    if (gx > 65535 || gy > 65535) return fail(GSR_ERR_UNSUPPORTED, "tile grid too large");
+    if (g->P == 0) return GSR_OK;
+    if (!g->means3D || (need_opacity && !g->opacities))
+        return fail(GSR_ERR_ARG, "means3D and opacities are required");
+    if ((g->shs == nullptr) == (g->colors_precomp == nullptr))
+        return fail(GSR_ERR_ARG, "Please provide excatly one of either SHs or precomputed colors!");
+    const bool sr = g->scales && g->rotations;
+    if (sr == (g->cov3D_precomp != nullptr) || ((g->scales != nullptr) != (g->rotations != nullptr)))
+        return fail(GSR_ERR_ARG, "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (g->shs && (g->sh_coeffs <= 0 || (g->sh_degree + 1) * (g->sh_degree + 1) > g->sh_coeffs || g->sh_degree > 3 || g->sh_degree < 0))
+        return fail(GSR_ERR_ARG, "invalid SH configuration: degree %d with %d coefficients", g->sh_degree, g->sh_coeffs);
+    if (!cam->viewmatrix || !cam->projmatrix || !cam->bg || (g->shs && !cam->campos))
+        return fail(GSR_ERR_ARG, "camera matrices / bg / campos missing");
+    return GSR_OK;
+}
+
+void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
+    memset(&a, 0, sizeof(a));
+    a.P = g->P; a.D = g->sh_degree; a.M = g->shs ? g->sh_coeffs : 0;
+    a.W = cam->image_width; a.H = cam->image_height;
+    a.gx = div_up(a.W, kTileW); a.gy = div_up(a.H, kTileH);
+    a.scale_modifier = g->scale_modifier;
+    a.tan_fovx = cam->tan_fovx; a.tan_fovy = cam->tan_fovy;
+    a.focal_y = a.H / (2.0f * a.tan_fovy);
+    a.focal_x = a.W / (2.0f * a.tan_fovx);
+    a.means3D = g->means3D; a.scales = g->scales; a.rotations = g->rotations; a.opacities = g->opacities;
+    a.shs = g->shs; a.colors_precomp = g->colors_precomp; a.cov3D_precomp = g->cov3D_precomp;
+    a.viewmatrix = cam->viewmatrix; a.projmatrix = cam->projmatrix; a.campos = cam->campos; a.bg = cam->bg;
+}
+
+void carve_geom(FwdArgs &a, char *base) {
+    const GeomLayout L(a.P);
+    a.depth = (float *)(base + L.depth); a.xy = (float2 *)(base + L.xy);
+    a.conic_op = (float4 *)(base + L.conic_op); a.rgbd = (float4 *)(base + L.rgbd);
+    a.rect = (uint2 *)(base + L.rect); a.tiles = (uint32_t *)(base + L.tiles); a.goff = (uint32_t *)(base + L.goff);
+}
+void carve_image(FwdArgs &a, char *base) {
+    const ImageLayout L(a.W, a.H, a.P);
+    a.ranges = (uint2 *)(base + L.ranges); a.final_T = (float *)(base + L.final_T);
+    a.n_contrib = (uint32_t *)(base + L.n_contrib); a.tile_maxc = (uint32_t *)(base + L.tile_maxc);
+    a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
+    a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
+    a.meta = (uint32_t *)(base + L.meta);
+}
+void carve_binning(FwdArgs &a, char *base, int K) {
+    const BinningLayout L(K);
+    a.keys = (uint64_t *)(base + L.keys); a.point_list = (uint32_t *)(base + L.point_list);
+    a.inv = (uint32_t *)(base + L.inv);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *gsr_last_error(void) { return g_err.c_str(); }
+int gsr_abi_version(void) { return GSR_ABI_VERSION; }
+
+size_t gsr_geom_bytes(int P) { return GeomLayout(P < 0 ? 0 : P).total; }
+size_t gsr_image_bytes(int W, int H, int P) { return ImageLayout(W, H, P < 0 ? 0 : P).total; }
+size_t gsr_binning_bytes(int K) { return BinningLayout(K).total; }
+size_t gsr_scratch_bytes(int K) { return ScratchLayout(K).total; }
+
+int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
+    const GeomLayout g(P);
+    const ImageLayout im(W, H, P);
+    const BinningLayout b(K);
+    const size_t v[14] = {g.depth, g.xy, g.conic_op, g.rgbd, g.rect, g.tiles, g.goff,
+                          im.ranges, im.final_T, im.n_contrib, im.tile_maxc,
+                          b.keys, b.point_list, b.inv};
+    int n = 0;
+    for (; n < 14 && n < max_out; ++n) out[n] = v[n];
+    return n;
+}
+
+int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                float *out_color, float *out_depth, int *out_radii, int *out_num_rendered,
+                void *stream) {
+    int rc = check_common(cam, g, true);
+    if (rc) return rc;
+    if (!alloc || !out_color || !out_depth || !out_num_rendered || (g->P > 0 && !out_radii))
+        return fail(GSR_ERR_ARG, "gsr_forward: missing output or allocator");
+    hipStream_t s = (hipStream_t)stream;
+    FwdArgs a;
+    fill_common(a, cam, g);
+    a.radii = out_radii; a.out_color = out_color; a.out_depth = out_depth;
+    const size_t npix = (size_t)a.W * a.H;
+    // The three persistent buffers are always requested, so a caller can hand them back verbatim.
+    char *geom = (char *)alloc(alloc_ctx, GSR_BUF_GEOM, GeomLayout(a.P).total);
+    char *img = (char *)alloc(alloc_ctx, GSR_BUF_IMAGE, ImageLayout(a.W, a.H, a.P).total);
+    if (!geom || !img) return fail(GSR_ERR_ALLOC, "allocation callback failed (geom/image)");
+    carve_geom(a, geom);
+    carve_image(a, img);
+    *out_num_rendered = 0;
+    if (a.P == 0) {  // reference: colour/depth stay zero (no background) when there are no Gaussians
+        HIP_TRY(launch_zero(out_color, 3 * npix, s));
+        HIP_TRY(launch_zero(out_depth, npix, s));
+        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout(0).total);
+        if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning)");
+        return GSR_OK;
+    }
+    { Phase ph(s, "preprocess"); HIP_TRY(launch_preprocess(a, s)); }
+    { Phase ph(s, "bin_count"); HIP_TRY(launch_bin_count(a, s)); }
+    { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, s)); }
+    uint32_t *hw = pinned_word();
+    if (!hw) return fail(GSR_ERR_HIP, "hipHostMalloc failed");
+    HIP_TRY(hipMemcpyAsync(hw, a.meta, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint32_t K = hw[0];
+    if (K > 0x7FFFFFFFu) return fail(GSR_ERR_UNSUPPORTED, "num_rendered overflow");
+    *out_num_rendered = (int)K;
+    char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)K).total);
+    if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
+    carve_binning(a, bin, (int)K);
+    { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, (int)K, s)); }
+    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, s)); }
+    { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
+    return GSR_OK;
+}
+
+int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
+                 const void *geom, const void *binning, const void *image, const float *dL_dcolor,
+                 const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
+                 void *stream) {
+    (void)dL_ddepth;
+    int rc = check_common(cam, g, false);
+    if (rc) return rc;
+    if (!out) return fail(GSR_ERR_ARG, "gsr_backward: null grads");
+    if (g->P == 0) return GSR_OK;
+    if (!geom || !binning || !image || !dL_dcolor || !radii || !alloc)
+        return fail(GSR_ERR_ARG, "gsr_backward: missing saved buffers / dL_dcolor / allocator");
+    if (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dopacity || !out->dL_dmeans3D ||
+        !out->dL_dcov3D || !out->dL_dscales || !out->dL_drotations || (g->shs && !out->dL_dsh))
+        return fail(GSR_ERR_ARG, "gsr_backward: missing gradient output");
+    if (num_rendered < 0) return fail(GSR_ERR_ARG, "num_rendered < 0");
+    hipStream_t s = (hipStream_t)stream;
+    FwdArgs f;
+    fill_common(f, cam, g);
+    carve_geom(f, (char *)geom);
+    carve_image(f, (char *)image);
+    carve_binning(f, (char *)binning, num_rendered);
+    BwdArgs a;
+    memset(&a, 0, sizeof(a));
+    a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
+    a.scale_modifier = f.scale_modifier; a.tan_fovx = f.tan_fovx; a.tan_fovy = f.tan_fovy;
+    a.focal_x = f.focal_x; a.focal_y = f.focal_y;
+    a.means3D = f.means3D; a.scales = f.scales; a.rotations = f.rotations; a.shs = f.shs;
+    a.colors_precomp = f.colors_precomp; a.cov3D_precomp = f.cov3D_precomp;
+    a.viewmatrix = f.viewmatrix; a.projmatrix = f.projmatrix; a.campos = f.campos; a.bg = f.bg;
+    a.radii = radii;
+    a.xy = f.xy; a.conic_op = f.conic_op; a.rgbd = f.rgbd; a.rect = f.rect; a.goff = f.goff;
+    a.ranges = f.ranges; a.final_T = f.final_T; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
+    a.point_list = f.point_list; a.inv = f.inv;
+    a.dL_dcolor = dL_dcolor;
+    a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
+    a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = out->dL_dsh;
+    a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
+    char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, ScratchLayout(num_rendered).total);
+    if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
+    a.partial = (float *)scr;
+    { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
+    { Phase ph(s, "gauss_bwd"); HIP_TRY(launch_gauss_bwd(a, s)); }
+    return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream) {
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_ERR_ARG, "P must be >= 0");
+    if (P > 0 && (!means3D || !viewmatrix || !present)) return fail(GSR_ERR_ARG, "null pointer");
+    HIP_TRY(launch_mark_visible(P, means3D, viewmatrix, present, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+int gsr_profile_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+    return GSR_OK;
+}
+
+int gsr_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    for (auto &r : g_prof) { g_evpool.push_back(r.a); g_evpool.push_back(r.b); }
+    g_prof.clear();
+    return GSR_OK;
+}
+
+int gsr_profile_read(const char *phase, double *total_ms, int *count) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    double tot = 0; int n = 0;
+    for (auto &r : g_prof) {
+        if (phase && r.phase != phase) continue;
+        if (hipEventSynchronize(r.b) != hipSuccess) return fail(GSR_ERR_HIP, "hipEventSynchronize failed");
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) return fail(GSR_ERR_HIP, "hipEventElapsedTime failed");
+        tot += ms; ++n;
+    }
+    if (total_ms) *total_ms = tot;
+    if (count) *count = n;
+    return GSR_OK;
+}
+
+}  // extern "C"

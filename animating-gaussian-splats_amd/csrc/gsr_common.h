@@ -1,0 +1,271 @@
+// gsr_common.h -- shared device math, constants and HBM workspace layouts of libgsr.
+//
+// The float expressions below are evaluated in exactly the order the CPU oracle
+// (oracle/gsr_oracle.c) evaluates them, and the library is compiled with -ffp-contract=off, so
+// every float that feeds an integer decision (radius, tile rectangle, sort key) is bit-identical to
+// the oracle.  Behavioural spec: SURVEY.md section 2.1 (upstream diff-gaussian-rasterization-w-depth,
+// absent from /root/reference: .gitmodules:1-3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+constexpr int kTileW = 16;  // 16x16 pixel tiles (upstream BLOCK_X/BLOCK_Y)
+constexpr int kTileH = 16;
+constexpr int kTilePix = kTileW * kTileH;  // 256 = 4 wave64 per tile block
+constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic xyw, dopacity, dcolor rgb
+constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
+
+__host__ __device__ inline int div_up(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// ---------------------------------------------------------------------------------------------
+// Workspace layouts.  One allocation per kind; every array starts 256-byte aligned.
+// ---------------------------------------------------------------------------------------------
+// GEOM (per Gaussian, P): SoA arrays written by preprocess, read by binning/render/backward.
+struct GeomLayout {
+    size_t depth, xy, conic_op, rgbd, rect, tiles, goff, total;
+    __host__ __device__ GeomLayout(int P) {
+        size_t o = 0;
+        depth = o;    o = align256(o + sizeof(float) * P);
+        xy = o;       o = align256(o + sizeof(float2) * P);
+        conic_op = o; o = align256(o + sizeof(float4) * P);
+        rgbd = o;     o = align256(o + sizeof(float4) * P);
+        rect = o;     o = align256(o + sizeof(uint2) * P);
+        tiles = o;    o = align256(o + sizeof(uint32_t) * P);
+        goff = o;     o = align256(o + sizeof(uint32_t) * (P + 1));
+        total = o;
+    }
+};
+
+// Binning work decomposition over Gaussians: NB chunks of CH Gaussians (CH multiple of 256).
+struct BinGrid {
+    int CH, NB;
+    __host__ __device__ BinGrid(int P) {
+        int c = div_up(P, 256);
+        c = div_up(c, 256) * 256;
+        CH = c < 1024 ? 1024 : c;
+        NB = P > 0 ? div_up(P, CH) : 0;
+    }
+};
+
+// IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
+struct ImageLayout {
+    size_t ranges, final_T, n_contrib, tile_maxc, tile_count, tile_cursor, block_sums, block_off,
+        meta, total;
+    __host__ __device__ ImageLayout(int W, int H, int P) {
+        const int T = div_up(W, kTileW) * div_up(H, kTileH);
+        const int N = W * H;
+        const int NB = BinGrid(P).NB;
+        size_t o = 0;
+        ranges = o;      o = align256(o + sizeof(uint2) * T);
+        final_T = o;     o = align256(o + sizeof(float) * N);
+        n_contrib = o;   o = align256(o + sizeof(uint32_t) * N);
+        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * T);
+        tile_count = o;  o = align256(o + sizeof(uint32_t) * T);
+        tile_cursor = o; o = align256(o + sizeof(uint32_t) * T);
+        block_sums = o;  o = align256(o + sizeof(uint32_t) * (NB + 1));
+        block_off = o;   o = align256(o + sizeof(uint32_t) * (NB + 1));
+        meta = o;        o = align256(o + sizeof(uint32_t) * 16);
+        total = o;
+    }
+};
+
+// BINNING (per Gaussian-tile pair, K): sort keys, sorted Gaussian list, emission -> slot map.
+struct BinningLayout {
+    size_t keys, point_list, inv, total;
+    __host__ __device__ BinningLayout(int K) {
+        size_t o = 0;
+        keys = o;       o = align256(o + sizeof(uint64_t) * (K > 0 ? K : 1));
+        point_list = o; o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
+        inv = o;        o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
+        total = o;
+    }
+};
+
+// SCRATCH (backward): one 9-float partial-gradient record per sorted slot.
+struct ScratchLayout {
+    size_t partial, total;
+    __host__ __device__ ScratchLayout(int K) {
+        partial = 0;
+        total = align256(sizeof(float) * kPartial * size_t(K > 0 ? K : 1));
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Device math -- same op order as oracle/gsr_oracle.c
+// ---------------------------------------------------------------------------------------------
+#define GSR_SH_C0 0.28209479177387814f
+#define GSR_SH_C1 0.4886025119029199f
+__device__ __constant__ const float kSH_C2[5] = {1.0925484305920792f, -1.0925484305920792f,
+                                                 0.31539156525252005f, -1.0925484305920792f,
+                                                 0.5462742152960396f};
+__device__ __constant__ const float kSH_C3[7] = {-0.5900435899266435f, 2.890611442640554f,
+                                                 -0.4570457994644658f, 0.3731763325901154f,
+                                                 -0.4570457994644658f, 1.445305721320277f,
+                                                 -0.5900435899266435f};
+
+// column-major 3x3 (glm storage): m[c*3+r]
+struct m3 { float m[9]; };
+#define GM(A, c, r) ((A).m[(c) * 3 + (r)])
+
+__device__ inline m3 m3_mul(const m3 &a, const m3 &b) {
+    m3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            o.m[c * 3 + r] = a.m[0 * 3 + r] * b.m[c * 3 + 0] + a.m[1 * 3 + r] * b.m[c * 3 + 1] +
+                             a.m[2 * 3 + r] * b.m[c * 3 + 2];
+    return o;
+}
+__device__ inline m3 m3_T(const m3 &a) {
+    m3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o.m[c * 3 + r] = a.m[r * 3 + c];
+    return o;
+}
+
+__device__ inline float ndc2pix(float v, int S) { return (float)(((v + 1.0) * S - 1.0) * 0.5); }
+
+__device__ inline void get_rect(float px, float py, int max_radius, int gx, int gy, int &x0, int &y0,
+                                int &x1, int &y1) {
+    x0 = min(gx, max(0, (int)((px - max_radius) / kTileW)));
+    y0 = min(gy, max(0, (int)((py - max_radius) / kTileH)));
+    x1 = min(gx, max(0, (int)((px + max_radius + kTileW - 1) / kTileW)));
+    y1 = min(gy, max(0, (int)((py + max_radius + kTileH - 1) / kTileH)));
+}
+
+__device__ inline float3 xform4x3(float3 p, const float *m) {
+    return make_float3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                       m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+__device__ inline float4 xform4x4(float3 p, const float *m) {
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                       m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14],
+                       m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+
+__device__ inline m3 rot_from_quat(float4 q) {  // q = (w, x, y, z), NOT normalised (reference quirk)
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    m3 R = {{1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+             2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+             2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)}};
+    return R;
+}
+
+__device__ inline void cov3d_from_scale_rot(float3 s3, float mod, float4 q, float *cov) {
+    m3 S = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
+    GM(S, 0, 0) = mod * s3.x; GM(S, 1, 1) = mod * s3.y; GM(S, 2, 2) = mod * s3.z;
+    const m3 R = rot_from_quat(q);
+    const m3 M = m3_mul(S, R);
+    const m3 Sig = m3_mul(m3_T(M), M);
+    cov[0] = GM(Sig, 0, 0); cov[1] = GM(Sig, 0, 1); cov[2] = GM(Sig, 0, 2);
+    cov[3] = GM(Sig, 1, 1); cov[4] = GM(Sig, 1, 2); cov[5] = GM(Sig, 2, 2);
+}
+
+__device__ inline float3 cov2d(float3 mean, float fx, float fy, float tfx, float tfy, const float *c3,
+                               const float *vm) {
+    float3 t = xform4x3(mean, vm);
+    const float limx = 1.3f * tfx, limy = 1.3f * tfy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const m3 J = {{fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z,
+                   -(fy * t.y) / (t.z * t.z), 0, 0, 0}};
+    const m3 Wm = {{vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]}};
+    const m3 T = m3_mul(Wm, J);
+    const m3 V = {{c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]}};
+    const m3 cov = m3_mul(m3_mul(m3_T(T), m3_T(V)), T);
+    return make_float3(GM(cov, 0, 0) + 0.3f, GM(cov, 0, 1), GM(cov, 1, 1) + 0.3f);
+}
+
+// SH -> RGB for one channel set; `sh` points at the Gaussian's (M,3) coefficients.
+__device__ inline float3 sh_to_rgb(int deg, float3 mean, const float *campos, const float *sh,
+                                   bool *clamped) {
+    float3 dir = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
+    const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
+    dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
+    float out[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+#define S(i) sh[(i) * 3 + ch]
+        float res = GSR_SH_C0 * S(0);
+        if (deg > 0) {
+            const float x = dir.x, y = dir.y, z = dir.z;
+            res = res - GSR_SH_C1 * y * S(1) + GSR_SH_C1 * z * S(2) - GSR_SH_C1 * x * S(3);
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                res = res + kSH_C2[0] * xy * S(4) + kSH_C2[1] * yz * S(5) +
+                      kSH_C2[2] * (2.0f * zz - xx - yy) * S(6) + kSH_C2[3] * xz * S(7) +
+                      kSH_C2[4] * (xx - yy) * S(8);
+                if (deg > 2) {
+                    res = res + kSH_C3[0] * y * (3.0f * xx - yy) * S(9) + kSH_C3[1] * xy * z * S(10) +
+                          kSH_C3[2] * y * (4.0f * zz - xx - yy) * S(11) +
+                          kSH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * S(12) +
+                          kSH_C3[4] * x * (4.0f * zz - xx - yy) * S(13) +
+                          kSH_C3[5] * z * (xx - yy) * S(14) + kSH_C3[6] * x * (xx - 3.0f * yy) * S(15);
+                }
+            }
+        }
+#undef S
+        res += 0.5f;
+        clamped[ch] = res < 0;
+        out[ch] = res < 0.0f ? 0.0f : res;
+    }
+    return make_float3(out[0], out[1], out[2]);
+}
+
+// rect packing: x = x0 | y0 << 16, y = x1 | y1 << 16
+__device__ inline uint2 pack_rect(int x0, int y0, int x1, int y1) {
+    return make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
+}
+
+// ---------------------------------------------------------------------------------------------
+// wave64 / block primitives
+// ---------------------------------------------------------------------------------------------
+__device__ inline uint32_t wave_incl_scan_u32(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+// Block-wide exclusive scan over blockDim.x (multiple of 64, <= 1024); `lds` holds >= 16 words.
+// Returns the exclusive prefix; *total receives the block sum.  Contains __syncthreads().
+__device__ inline uint32_t block_excl_scan_u32(uint32_t v, uint32_t *lds, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t inc = wave_incl_scan_u32(v);
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    uint32_t woff = 0, tot = 0;
+    for (int w = 0; w < nw; ++w) {
+        const uint32_t s = lds[w];
+        if (w < wid) woff += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return woff + inc - v;
+}
+
+// Sum of v over the 64 lanes of the wave, valid in lane 63 (gfx9 DPP row ops + row broadcasts).
+__device__ inline float wave_sum_lane63(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false)); // row_bcast:15
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false)); // row_bcast:31
+    return v;
+}
+
+}  // namespace gsr

@@ -1,0 +1,455 @@
+// gsr_forward.hip -- forward pass of the MI355X-native Gaussian-splat rasterizer.
+//
+// Pipeline (one HIP stream, one host sync for the pair count K, as the reference does):
+//   k_preprocess   1 thread / Gaussian: cull, Sigma3D, EWA Sigma2D, conic, radius, tile rect, SH->RGB
+//   k_bin_count    chunked over Gaussians: LDS tile histogram -> one global add per (chunk, tile)
+//   k_bin_scan     1 block: exclusive scan of tile counts -> tile ranges; scan of chunk sums; K
+//   k_bin_emit     chunked: re-count in LDS, reserve a (chunk, tile) slab, scatter 64-bit keys
+//                  (depth_bits << 32 | gaussian) into their tile's range; exclusive emission offsets
+//   k_tile_sort    1 block / tile: sort the tile's keys by (depth bits, index) in LDS (bitonic),
+//                  write the Gaussian list + the emission->slot map used by the backward reduction
+//   k_render_fwd   1 block (4 wave64) / 16x16 tile: front-to-back blend of colour and depth
+//
+// The reference instead emits (tile<<32 | depth) keys and radix-sorts all K pairs globally
+// (SURVEY.md 2.1 rows duplicateWithKeys / SortPairs / identifyTileRanges).  Bucketing by tile first
+// and sorting (depth, index) inside each tile yields the identical order: a stable LSD sort on
+// (tile, depth) breaks ties by emission order, and within one tile the emission order is the
+// Gaussian index.  Tile ranges fall out of the bucket scan.
+#include "gsr_common.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_preprocess(
+    int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales,
+    float scale_modifier, const float *__restrict__ rotations, const float *__restrict__ opacities,
+    const float *__restrict__ shs, const float *__restrict__ colors_precomp,
+    const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
+    const float *__restrict__ projmatrix, const float *__restrict__ campos, int W, int H,
+    float tan_fovx, float tan_fovy, float focal_x, float focal_y, int gx, int gy,
+    int *__restrict__ radii, float *__restrict__ depth_out, float2 *__restrict__ xy_out,
+    float4 *__restrict__ conic_op_out, float4 *__restrict__ rgbd_out, uint2 *__restrict__ rect_out,
+    uint32_t *__restrict__ tiles_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    // matrices are tiny and uniform: every lane reads the same words (scalar loads)
+    float vm[16], pm[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { vm[k] = viewmatrix[k]; pm[k] = projmatrix[k]; }
+    radii[i] = 0;
+    tiles_out[i] = 0;
+    rect_out[i] = make_uint2(0, 0);
+    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    const float4 ph = xform4x4(p, pm);
+    const float3 pv = xform4x3(p, vm);
+    if (pv.z <= 0.2f) return;  // near-plane cull (in_frustum)
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float ppx = ph.x * pw, ppy = ph.y * pw;
+    float c3[6];
+    if (cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = cov3D_precomp[6 * i + k];
+    } else {
+        const float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+        const float4 q = make_float4(rotations[4 * i], rotations[4 * i + 1], rotations[4 * i + 2],
+                                     rotations[4 * i + 3]);
+        cov3d_from_scale_rot(s, scale_modifier, q, c3);
+    }
+    const float3 cv = cov2d(p, focal_x, focal_y, tan_fovx, tan_fovy, c3, vm);
+    const float det = cv.x * cv.z - cv.y * cv.y;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float mid = 0.5f * (cv.x + cv.z);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+    const float pix_x = ndc2pix(ppx, W), pix_y = ndc2pix(ppy, H);
+    int x0, y0, x1, y1;
+    get_rect(pix_x, pix_y, (int)my_radius, gx, gy, x0, y0, x1, y1);
+    if ((x1 - x0) * (y1 - y0) == 0) return;
+    float3 rgb;
+    if (colors_precomp) {
+        rgb = make_float3(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2]);
+    } else {
+        bool cl[3];
+        rgb = sh_to_rgb(D, p, campos, shs + (size_t)i * M * 3, cl);
+    }
+    radii[i] = (int)my_radius;
+    depth_out[i] = pv.z;
+    xy_out[i] = make_float2(pix_x, pix_y);
+    conic_op_out[i] = make_float4(cv.z * det_inv, -cv.y * det_inv, cv.x * det_inv, opacities[i]);
+    rgbd_out[i] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
+    rect_out[i] = pack_rect(x0, y0, x1, y1);
+    tiles_out[i] = (uint32_t)((y1 - y0) * (x1 - x0));
+}
+
+// ------------------------------------------------------------------------------------------
+// Tile histogram per chunk of Gaussians.  USE_LDS: histogram in LDS (T <= kMaxLdsTiles), then one
+// global atomic per non-empty (chunk, tile) bin -- lanes of a wave add to 64 consecutive counters.
+template <bool USE_LDS>
+__global__ __launch_bounds__(256) void k_bin_count(int P, int CH, int T, int gx,
+                                                   const uint2 *__restrict__ rects,
+                                                   const uint32_t *__restrict__ tiles,
+                                                   uint32_t *__restrict__ tile_count,
+                                                   uint32_t *__restrict__ block_sums) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
+    __shared__ uint32_t s_red[16];
+    const int b = blockIdx.x;
+    const int g0 = b * CH, g1 = min(P, g0 + CH);
+    if (USE_LDS) {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) s_hist[t] = 0;
+        __syncthreads();
+    }
+    uint32_t my_sum = 0;
+    for (int g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
+        const uint32_t n = tiles[g];
+        if (n == 0) continue;
+        my_sum += n;
+        const uint2 r = rects[g];
+        const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+        for (int y = y0; y < y1; ++y)
+            for (int x = x0; x < x1; ++x) {
+                if (USE_LDS) atomicAdd(&s_hist[y * gx + x], 1u);
+                else atomicAdd(&tile_count[y * gx + x], 1u);
+            }
+    }
+    uint32_t tot;
+    block_excl_scan_u32(my_sum, s_red, &tot);
+    if (threadIdx.x == 0) block_sums[b] = tot;
+    if (USE_LDS) {
+        __syncthreads();
+        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+            const uint32_t c = s_hist[t];
+            if (c) atomicAdd(&tile_count[t], c);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Single block (1024 threads): exclusive scan of the T tile counts -> ranges/cursors, and of the
+// NB chunk sums -> chunk emission offsets.  meta[0] = K.
+__global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t *__restrict__ tile_count,
+                                                   uint2 *__restrict__ ranges,
+                                                   uint32_t *__restrict__ tile_cursor,
+                                                   const uint32_t *__restrict__ block_sums,
+                                                   uint32_t *__restrict__ block_off,
+                                                   uint32_t *__restrict__ meta) {
+    __shared__ uint32_t s_red[16];
+    uint32_t carry = 0;
+    for (int base = 0; base < T; base += blockDim.x) {
+        const int t = base + threadIdx.x;
+        const uint32_t c = t < T ? tile_count[t] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32(c, s_red, &tot) + carry;
+        if (t < T) {
+            ranges[t] = c ? make_uint2(ex, ex + c) : make_uint2(0, 0);  // empty tiles: {0,0} like the reference
+            tile_cursor[t] = ex;
+        }
+        carry += tot;
+    }
+    uint32_t carry2 = 0;
+    for (int base = 0; base < NB; base += blockDim.x) {
+        const int b = base + threadIdx.x;
+        const uint32_t c = b < NB ? block_sums[b] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32(c, s_red, &tot) + carry2;
+        if (b < NB) block_off[b] = ex;
+        carry2 += tot;
+    }
+    if (threadIdx.x == 0) meta[0] = carry;
+}
+
+// ------------------------------------------------------------------------------------------
+// Scatter keys into tile buckets.  Each chunk re-counts its tile histogram in LDS, reserves one
+// contiguous slab per non-empty tile with a single global atomic, then hands out slots from LDS.
+// The order inside a tile is arbitrary here; k_tile_sort makes it canonical.
+template <bool USE_LDS>
+__global__ __launch_bounds__(256) void k_bin_emit(int P, int CH, int T, int gx,
+                                                  const uint2 *__restrict__ rects,
+                                                  const uint32_t *__restrict__ tiles,
+                                                  const float *__restrict__ depth,
+                                                  const uint32_t *__restrict__ block_off,
+                                                  uint32_t *__restrict__ tile_cursor,
+                                                  uint32_t *__restrict__ goff,
+                                                  uint64_t *__restrict__ keys, uint32_t K) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
+    __shared__ uint32_t s_red[16];
+    const int b = blockIdx.x;
+    const int g0 = b * CH, g1 = min(P, g0 + CH);
+    if (USE_LDS) {
+        for (int t = threadIdx.x; t < T; t += blockDim.x) s_cur[t] = 0;
+        __syncthreads();
+        for (int g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
+            if (tiles[g] == 0) continue;
+            const uint2 r = rects[g];
+            const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+            for (int y = y0; y < y1; ++y)
+                for (int x = x0; x < x1; ++x) atomicAdd(&s_cur[y * gx + x], 1u);
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < T; t += blockDim.x) {
+            const uint32_t c = s_cur[t];
+            s_cur[t] = c ? atomicAdd(&tile_cursor[t], c) : 0u;
+        }
+        __syncthreads();
+    }
+    // emission offsets (exclusive scan of tiles over Gaussian index) + key scatter
+    uint32_t carry = block_off[b];
+    for (int base = g0; base < g1; base += blockDim.x) {
+        const int g = base + threadIdx.x;
+        const uint32_t n = g < g1 ? tiles[g] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32(n, s_red, &tot) + carry;
+        carry += tot;
+        if (g < g1) {
+            goff[g] = ex;
+            if (n) {
+                const uint2 r = rects[g];
+                const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+                const uint64_t key_lo = (uint64_t)(uint32_t)g;
+                const uint64_t key = ((uint64_t)__float_as_uint(depth[g]) << 32) | key_lo;
+                for (int y = y0; y < y1; ++y)
+                    for (int x = x0; x < x1; ++x) {
+                        const int t = y * gx + x;
+                        const uint32_t pos = USE_LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_cursor[t], 1u);
+                        keys[pos] = key;
+                    }
+            }
+        }
+    }
+    if (b == gridDim.x - 1 && threadIdx.x == 0) goff[P] = K;
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-tile sort of (depth_bits << 32 | index) keys, then outputs.
+__device__ inline void tile_sort_write(uint64_t key, uint32_t slot, int tx, int ty,
+                                       const uint2 *__restrict__ rects,
+                                       const uint32_t *__restrict__ goff,
+                                       uint32_t *__restrict__ point_list, uint32_t *__restrict__ inv) {
+    const uint32_t g = (uint32_t)key;
+    point_list[slot] = g;
+    const uint2 r = rects[g];
+    const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF;
+    inv[goff[g] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0))] = slot;  // y-major emission order
+}
+
+__global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restrict__ ranges,
+                                                   uint64_t *__restrict__ keys,
+                                                   const uint2 *__restrict__ rects,
+                                                   const uint32_t *__restrict__ goff,
+                                                   uint32_t *__restrict__ point_list,
+                                                   uint32_t *__restrict__ inv) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
+    const int tile = blockIdx.x;
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (n <= 0) return;
+    const int tx = tile % gx, ty = tile / gx;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (n <= kSortCap) {
+        int np = 1;
+        while (np < n) np <<= 1;
+        for (int i = tid; i < np; i += nt) s_keys[i] = i < n ? keys[rg.x + i] : ~0ull;
+        __syncthreads();
+        for (int k = 2; k <= np; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < (np >> 1); i += nt) {
+                    const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+                    const bool asc = (lo & k) == 0;
+                    const uint64_t a = s_keys[lo], c = s_keys[hi];
+                    if ((a > c) == asc) { s_keys[lo] = c; s_keys[hi] = a; }
+                }
+                __syncthreads();
+            }
+        for (int i = tid; i < n; i += nt) tile_sort_write(s_keys[i], rg.x + i, tx, ty, rects, goff, point_list, inv);
+    } else {
+        // long tile: in-place bitonic network in global memory with virtual +inf padding
+        // ("flip" form: every comparator puts the minimum at the lower index).
+        uint64_t *a = keys + rg.x;
+        int np = 1;
+        while (np < n) np <<= 1;
+        for (int k = 2; k <= np; k <<= 1) {
+            const int h = k >> 1;
+            for (int i = tid; i < (np >> 1); i += nt) {
+                const int lo = ((i & ~(h - 1)) << 1) | (i & (h - 1)), hi = lo ^ (k - 1);
+                if (hi < n) {
+                    const uint64_t x = a[lo], y = a[hi];
+                    if (x > y) { a[lo] = y; a[hi] = x; }
+                }
+            }
+            __syncthreads();
+            for (int j = k >> 2; j > 0; j >>= 1) {
+                for (int i = tid; i < (np >> 1); i += nt) {
+                    const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
+                    if (hi < n) {
+                        const uint64_t x = a[lo], y = a[hi];
+                        if (x > y) { a[lo] = y; a[hi] = x; }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (int i = tid; i < n; i += nt) tile_sort_write(a[i], rg.x + i, tx, ty, rects, goff, point_list, inv);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Front-to-back blend, one 16x16 tile per 256-thread block (4 wave64: each wave = 4 pixel rows).
+// Gaussians are staged through LDS in batches of 256: xy, conic+opacity, rgb+depth (40 B each).
+__global__ __launch_bounds__(256) void k_render_fwd(
+    int W, int H, int gx, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list,
+    const float2 *__restrict__ xy, const float4 *__restrict__ conic_op, const float4 *__restrict__ rgbd,
+    const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
+    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc) {
+    __shared__ float2 s_xy[kTilePix];
+    __shared__ float4 s_co[kTilePix];
+    __shared__ float4 s_cd[kTilePix];
+    __shared__ uint32_t s_max;
+    const int tile = blockIdx.x;
+    const int tx = tile % gx, ty = tile / gx;
+    const int tid = threadIdx.x;
+    const int px = tx * kTileW + (tid & 15), py = ty * kTileH + (tid >> 4);
+    const bool inside = px < W && py < H;
+    const float pfx = (float)px, pfy = (float)py;
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    if (tid == 0) s_max = 0;
+    bool done = !inside;
+    float T = 1.0f, C0 = 0, C1 = 0, C2 = 0, Dp = 0;
+    uint32_t contributor = 0, last = 0;
+    for (int base = 0; base < n; base += kTilePix) {
+        if (__syncthreads_count(done) == kTilePix) break;
+        const int idx = base + tid;
+        if (idx < n) {
+            const uint32_t g = point_list[rg.x + idx];
+            s_xy[tid] = xy[g];
+            s_co[tid] = conic_op[g];
+            s_cd[tid] = rgbd[g];
+        }
+        __syncthreads();
+        const int cnt = min(kTilePix, n - base);
+        for (int j = 0; !done && j < cnt; ++j) {
+            ++contributor;
+            const float2 q = s_xy[j];
+            const float dx = q.x - pfx, dy = q.y - pfy;
+            const float4 co = s_co[j];
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            if (power > 0.0f) continue;
+            const float alpha = fminf(0.99f, co.w * expf(power));
+            if (alpha < 1.0f / 255.0f) continue;
+            const float test_T = T * (1 - alpha);
+            if (test_T < 0.0001f) { done = true; continue; }
+            const float4 cd = s_cd[j];
+            C0 += cd.x * alpha * T;
+            C1 += cd.y * alpha * T;
+            C2 += cd.z * alpha * T;
+            Dp += cd.w * alpha * T;
+            T = test_T;
+            last = contributor;
+        }
+    }
+    if (inside) {
+        const int pid = py * W + px;
+        final_T[pid] = T;
+        n_contrib[pid] = last;
+        out_color[pid] = C0 + T * bg[0];
+        out_color[H * W + pid] = C1 + T * bg[1];
+        out_color[2 * H * W + pid] = C2 + T * bg[2];
+        out_depth[pid] = Dp;
+    }
+    __syncthreads();
+    if (last) atomicMax(&s_max, last);
+    __syncthreads();
+    if (tid == 0) tile_maxc[tile] = s_max;
+}
+
+__global__ void k_zero_f32(float *p, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0.f;
+}
+
+__global__ void k_mark_visible(int P, const float *__restrict__ means3D,
+                               const float *__restrict__ viewmatrix, uint8_t *__restrict__ present) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    float vm[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) vm[k] = viewmatrix[k];
+    const float3 pv = xform4x3(make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]), vm);
+    present[i] = !(pv.z <= 0.2f);
+}
+
+// ==========================================================================================
+// host launchers
+// ==========================================================================================
+hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {
+    if (a.P == 0) return hipSuccess;
+    k_preprocess<<<div_up(a.P, 256), 256, 0, s>>>(
+        a.P, a.D, a.M, a.means3D, a.scales, a.scale_modifier, a.rotations, a.opacities, a.shs,
+        a.colors_precomp, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
+        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.xy, a.conic_op, a.rgbd,
+        a.rect, a.tiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
+    const BinGrid bg(a.P);
+    const int T = a.gx * a.gy;
+    hipError_t e = hipMemsetAsync(a.tile_count, 0, sizeof(uint32_t) * T, s);
+    if (e != hipSuccess) return e;
+    if (bg.NB == 0) return hipSuccess;
+    if (T <= kMaxLdsTiles)
+        k_bin_count<true><<<bg.NB, 256, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
+    else
+        k_bin_count<false><<<bg.NB, 256, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_scan(const FwdArgs &a, hipStream_t s) {
+    const BinGrid bg(a.P);
+    k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
+                                  a.block_sums, a.block_off, a.meta);
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
+    const BinGrid bg(a.P);
+    const int T = a.gx * a.gy;
+    if (bg.NB == 0) return hipSuccess;
+    if (T <= kMaxLdsTiles)
+        k_bin_emit<true><<<bg.NB, 256, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, (uint32_t)K);
+    else
+        k_bin_emit<false><<<bg.NB, 256, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, (uint32_t)K);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s) {
+    const int T = a.gx * a.gy;
+    k_tile_sort<<<T, 256, sizeof(uint64_t) * kSortCap, s>>>(a.gx, a.ranges, a.keys, a.rect, a.goff,
+                                                            a.point_list, a.inv);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
+    const int T = a.gx * a.gy;
+    k_render_fwd<<<T, kTilePix, 0, s>>>(a.W, a.H, a.gx, a.ranges, a.point_list, a.xy, a.conic_op,
+                                        a.rgbd, a.bg, a.out_color, a.out_depth, a.final_T,
+                                        a.n_contrib, a.tile_maxc);
+    return hipGetLastError();
+}
+
+hipError_t launch_zero(float *p, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_zero_f32<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(p, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
+                               hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    k_mark_visible<<<div_up(P, 256), 256, 0, s>>>(P, means3D, viewmatrix, present);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

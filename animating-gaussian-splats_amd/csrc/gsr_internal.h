@@ -1,0 +1,61 @@
+// gsr_internal.h -- argument bundles and host launchers shared by the libgsr translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+// Tile histogram kept in LDS when T * 4 B fits in 64 KiB; larger tile grids (e.g. 4K frames)
+// count straight into global memory.
+constexpr int kMaxLdsTiles = 16384;
+
+struct FwdArgs {
+    // inputs
+    int P, D, M, W, H, gx, gy;
+    float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
+    const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
+    const float *viewmatrix, *projmatrix, *campos, *bg;
+    // geom
+    float *depth; float2 *xy; float4 *conic_op; float4 *rgbd; uint2 *rect; uint32_t *tiles; uint32_t *goff;
+    // image
+    uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc; uint32_t *tile_count;
+    uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
+    // binning
+    uint64_t *keys; uint32_t *point_list; uint32_t *inv;
+    // outputs
+    int *radii; float *out_color; float *out_depth;
+};
+
+struct BwdArgs {
+    int P, D, M, W, H, gx, gy, K;
+    float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
+    const float *means3D, *scales, *rotations, *shs, *colors_precomp, *cov3D_precomp;
+    const float *viewmatrix, *projmatrix, *campos, *bg;
+    const int *radii;
+    // saved state
+    const float2 *xy; const float4 *conic_op; const float4 *rgbd; const uint2 *rect;
+    const uint32_t *goff; const uint2 *ranges; const float *final_T; const uint32_t *n_contrib;
+    const uint32_t *tile_maxc; const uint32_t *point_list; const uint32_t *inv;
+    // scratch
+    float *partial;
+    // upstream gradient
+    const float *dL_dcolor;
+    // outputs
+    float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
+        *dL_drot;
+};
+
+hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);
+hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s);
+hipError_t launch_bin_scan(const FwdArgs &a, hipStream_t s);
+hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s);
+hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s);
+hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s);
+hipError_t launch_zero(float *p, size_t n, hipStream_t s);
+hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
+                               hipStream_t s);
+
+hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
+hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
+
+}  // namespace gsr

@@ -1,0 +1,273 @@
+"""Native entry points of the drop-in rasterizer, bound over the C ABI of ``libgsr.so``.
+
+Same three names, argument order and return tuples as the reference extension's pybind module
+``diff_gaussian_rasterization._C`` (``ext.cpp`` / ``rasterize_points.cu`` of the
+diff-gaussian-rasterization-w-depth submodule, ``/root/reference/.gitmodules:1-3``):
+
+* ``rasterize_gaussians(...) -> (num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth)``
+* ``rasterize_gaussians_backward(...) -> (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D,
+  dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)``
+* ``mark_visible(means3D, viewmatrix, projmatrix) -> bool[P]``
+
+Tensors cross the boundary as raw device pointers (``include/gsr.h``); the three persistent
+workspaces are ``torch.uint8`` tensors allocated through a ctypes callback so their lifetime follows
+the autograd graph, like the reference's ``resizeFunctional`` byte buffers.  There is no CPU path:
+a missing ``libgsr.so`` or a CPU tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSR_LIB", os.path.join(_HERE, "libgsr.so"))
+
+GSR_BUF_GEOM, GSR_BUF_BINNING, GSR_BUF_IMAGE, GSR_BUF_SCRATCH = 0, 1, 2, 3
+EXPORTED_SYMBOLS = (
+    "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_bytes", "gsr_image_bytes",
+    "gsr_binning_bytes", "gsr_scratch_bytes", "gsr_last_error", "gsr_abi_version",
+    "gsr_profile_enable", "gsr_profile_reset", "gsr_profile_read", "gsr_buffer_offsets",
+)
+
+
+class _Camera(ctypes.Structure):
+    _fields_ = [("image_width", ctypes.c_int), ("image_height", ctypes.c_int),
+                ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float),
+                ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
+                ("campos", ctypes.c_void_p), ("bg", ctypes.c_void_p),
+                ("prefiltered", ctypes.c_int)]
+
+
+class _Gaussians(ctypes.Structure):
+    _fields_ = [("P", ctypes.c_int), ("sh_degree", ctypes.c_int), ("sh_coeffs", ctypes.c_int),
+                ("scale_modifier", ctypes.c_float), ("means3D", ctypes.c_void_p),
+                ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
+                ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
+                ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p)]
+
+
+class _Grads(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
+        "dL_dscales", "dL_drotations")]
+
+
+_ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
+_lib = None
+
+
+def load_library():
+    """Load ``libgsr.so`` (raises if it has not been built: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libgsr.so not found at {LIB_PATH}: build it with `make -C animating-gaussian-splats_amd/csrc` "
+            "(or __graft_entry__.build()); the rasterizer has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.gsr_forward.restype = i
+    L.gsr_forward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), _ALLOC_FN, vp,
+                              vp, vp, vp, ctypes.POINTER(i), vp]
+    L.gsr_backward.restype = i
+    L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
+                               vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]
+    L.gsr_mark_visible.restype = i
+    L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):
+        getattr(L, n).restype = ctypes.c_size_t
+        getattr(L, n).argtypes = [i]
+    L.gsr_image_bytes.restype = ctypes.c_size_t
+    L.gsr_image_bytes.argtypes = [i, i, i]
+    L.gsr_last_error.restype = ctypes.c_char_p
+    L.gsr_last_error.argtypes = []
+    L.gsr_abi_version.restype = i
+    L.gsr_profile_enable.argtypes = [i]
+    L.gsr_profile_enable.restype = i
+    L.gsr_profile_reset.restype = i
+    L.gsr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
+    L.gsr_profile_read.restype = i
+    L.gsr_buffer_offsets.restype = i
+    L.gsr_buffer_offsets.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_size_t), i]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc != 0:
+        msg = _lib.gsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"libgsr error {rc}: {msg}")
+
+
+def _ptr(t):
+    """Device pointer of a tensor, or None for an absent (empty) argument."""
+    if t is None or t.numel() == 0:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("diff_gaussian_rasterization: tensors must be on the GPU (no CPU path)")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"diff_gaussian_rasterization: expected float32, got {t.dtype}")
+    return t.data_ptr()
+
+
+def _f32(t):
+    return t.contiguous() if t is not None and t.numel() else t
+
+
+class _Allocator:
+    """ctypes allocation callback handing out torch byte tensors on the current device."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buffers = {}
+        self.cb = _ALLOC_FN(self._alloc)
+
+    def _alloc(self, _ctx, which, nbytes):
+        try:
+            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+        except Exception:  # noqa: BLE001 - reported through the C ABI as GSR_ERR_ALLOC
+            return None
+        self.buffers[int(which)] = t
+        return t.data_ptr()
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, campos, bg,
+            prefiltered, keep):
+    vm, pm = viewmatrix.contiguous().float(), projmatrix.contiguous().float()
+    bg_ = bg.contiguous().float()
+    cp = campos.contiguous().float() if campos is not None and campos.numel() else None
+    keep += [vm, pm, bg_, cp]
+    if vm.numel() != 16 or pm.numel() != 16:
+        raise RuntimeError("viewmatrix/projmatrix must hold 16 floats")
+    return _Camera(int(image_width), int(image_height), float(tan_fovx), float(tan_fovy),
+                   _ptr(vm), _ptr(pm), _ptr(cp) if cp is not None else None,
+                   _ptr(bg_), int(bool(prefiltered)))
+
+
+def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier, cov3D, keep):
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    P = means3D.size(0)
+    ts = [_f32(x) for x in (means3D, sh, colors, opacity, scales, rotations, cov3D)]
+    keep += ts
+    means3D, sh, colors, opacity, scales, rotations, cov3D = ts
+    M = sh.size(1) if sh is not None and sh.numel() else 0
+    return _Gaussians(P, int(degree), M, float(scale_modifier), _ptr(means3D), _ptr(sh), _ptr(colors),
+                      _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(cov3D)), P, M
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
+                        image_width, sh, degree, campos, prefiltered, debug=False):
+    L = load_library()
+    keep = []
+    g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
+                         cov3D_precomp, keep)
+    cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, campos,
+                  background, prefiltered, keep)
+    dev = means3D.device
+    H, W = int(image_height), int(image_width)
+    color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    alloc = _Allocator(dev)
+    nr = ctypes.c_int(0)
+    _check(L.gsr_forward(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
+                         depth.data_ptr(), radii.data_ptr() if P else None, ctypes.byref(nr),
+                         _stream_ptr(dev)))
+    b = alloc.buffers
+    return nr.value, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations,
+                                 scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
+                                 tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
+                                 binningBuffer, imageBuffer, debug=False, dL_dout_depth=None):
+    L = load_library()
+    keep = []
+    g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
+                         rotations, scale_modifier, cov3D_precomp, keep)
+    H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
+    cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
+    dev = means3D.device
+    e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731 - every element is written
+    out = (e(P, 3), e(P, 3), e(P, 1), e(P, 3), e(P, 6), e(P, M, 3), e(P, 3), e(P, 4))
+    if P == 0:
+        return out
+    dpix = dL_dout_color.contiguous().float()
+    keep.append(dpix)
+    grads = _Grads(*[t.data_ptr() if t.numel() else None for t in out])
+    alloc = _Allocator(dev)
+    _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
+                          geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+                          dpix.data_ptr(), None, alloc.cb, None, ctypes.byref(grads), _stream_ptr(dev)))
+    return out
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    L = load_library()
+    P = means3D.size(0)
+    present = torch.zeros((P,), dtype=torch.bool, device=means3D.device)
+    if P == 0:
+        return present
+    m = means3D.contiguous().float()
+    vm, pm = viewmatrix.contiguous().float(), projmatrix.contiguous().float()
+    _check(L.gsr_mark_visible(P, _ptr(m), _ptr(vm), _ptr(pm), present.data_ptr(),
+                              _stream_ptr(means3D.device)))
+    return present
+
+
+# ---- instrumentation (per-phase HIP-event timing inside libgsr) ----
+def profile_enable(on=True):
+    _check(load_library().gsr_profile_enable(int(bool(on))))
+
+
+def profile_reset():
+    _check(load_library().gsr_profile_reset())
+
+
+def profile_read(phase=None):
+    """Return (total_ms, count) of the recorded launches of ``phase`` (all phases if None)."""
+    L = load_library()
+    tot, cnt = ctypes.c_double(0), ctypes.c_int(0)
+    _check(L.gsr_profile_read(phase.encode() if phase else None, ctypes.byref(tot), ctypes.byref(cnt)))
+    return tot.value, cnt.value
+
+
+def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
+    """Typed views of the arrays inside the forward buffers (for parity tests / debugging)."""
+    L = load_library()
+    offs = (ctypes.c_size_t * 14)()
+    L.gsr_buffer_offsets(int(P), int(W), int(H), int(num_rendered), offs, 14)
+    o = list(offs)
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    K = int(num_rendered)
+
+    def view(buf, off, n, dtype, shape):
+        nbytes = n * torch.tensor([], dtype=dtype).element_size()
+        return buf[off:off + nbytes].view(dtype).reshape(shape)
+
+    f32, i32, i64 = torch.float32, torch.int32, torch.int64
+    return {
+        "depth": view(geomBuffer, o[0], P, f32, (P,)),
+        "xy": view(geomBuffer, o[1], 2 * P, f32, (P, 2)),
+        "conic_opacity": view(geomBuffer, o[2], 4 * P, f32, (P, 4)),
+        "rgbd": view(geomBuffer, o[3], 4 * P, f32, (P, 4)),
+        "rect": view(geomBuffer, o[4], 2 * P, i32, (P, 2)),
+        "tiles_touched": view(geomBuffer, o[5], P, i32, (P,)),
+        "goff": view(geomBuffer, o[6], P + 1, i32, (P + 1,)),
+        "ranges": view(imgBuffer, o[7], 2 * T, i32, (T, 2)),
+        "final_T": view(imgBuffer, o[8], W * H, f32, (H, W)),
+        "n_contrib": view(imgBuffer, o[9], W * H, i32, (H, W)),
+        "tile_maxc": view(imgBuffer, o[10], T, i32, (T,)),
+        "keys": view(binningBuffer, o[11], K, i64, (K,)),
+        "point_list": view(binningBuffer, o[12], K, i32, (K,)),
+        "inv": view(binningBuffer, o[13], K, i32, (K,)),
+    }

@@ -1,0 +1,211 @@
+"""Benchmark: differentiable Gaussian-splat rasterizer forward + backward (BASELINE.json metric).
+
+Metric: Msplats/s = P x views / wall-time(forward + backward) / 1e6, P counted pre-cull
+(SURVEY.md 8(d)).  Workload (BASELINE.json configs[2], the 1-GPU config the metric is quoted on):
+1M synthetic Gaussians, SH degree 3, 1920x1080, f = 1600, views from the 27-camera rig of
+configs[3] (heights {-0.8, 0, 0.8} x yaws {0, 40, ..., 320}).  One step = every rank renders
+``--views-per-rank`` views through the drop-in ``GaussianRasterizer`` (activations of
+shared.py:29-42 included), backpropagates a fixed upstream dL/dcolor into the leaf parameters
+(gradients accumulate over the rank's views, as train.py sums view losses), and for N > 1
+all-reduces (SUM) the parameter gradients over RCCL.  Inputs are resident in HBM before timing.
+
+N > 1: launched by torch.distributed.run, one process per GPU; rank r takes rig cameras
+(step * N * V + r * V + j) mod 27 (camera data parallelism, weak scaling: fixed views per GPU).
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events inside libgsr on
+the stream the kernel runs on) and the CPU-oracle baseline (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "animating-gaussian-splats_amd"), REPO]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def algorithmic_bytes(phase, P, K, N, T, F, sh):
+    """Compulsory HBM bytes of one launch of each kernel (DESIGN.md 'Kernels and their rooflines')."""
+    if phase == "preprocess":      # read means/scales/rot/opacity/features, write 7 SoA records
+        return P * (44 + F) + P * 60
+    if phase == "render_fwd":      # per pair: id + xy + conic/op + rgb/depth gather; per pixel outputs
+        return K * 44 + N * 24 + T * 12
+    if phase == "render_bwd":      # per pair: id + gathers + 36 B partial record; per pixel state
+        return K * (44 + 36) + N * 20 + T * 12
+    if phase == "gauss_bwd":       # per Gaussian inputs + all gradient outputs; per pair slot + record
+        return P * (44 + F + 12) + P * (56 + F) + K * 40
+    if phase == "tile_sort":       # keys in, point list + inverse map out, per-Gaussian rect/goff
+        return K * (8 + 4 + 4 + 12)
+    if phase == "bin_emit":
+        return P * 16 + K * 8
+    if phase == "bin_count":
+        return P * 12 + T * 4
+    return 0
+
+
+def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu):
+    """Single-threaded C oracle, forward + backward of ONE view of the same workload."""
+    from oracle import oracle as O
+    import splat_scenes as S
+    a = {k: (v.detach().numpy() if isinstance(v, torch.Tensor) else v)
+         for k, v in S.activated_inputs(params_cpu, cfg.sh_degree).items()}
+    t0 = time.perf_counter()
+    st = O.forward(cam_cpu.bg.numpy(), a["means3D"], a.get("colors_precomp"), a["opacities"],
+                   a["scales"], a["rotations"], 1.0, None, cam_cpu.viewmatrix, cam_cpu.projmatrix,
+                   cam_cpu.tanfovx, cam_cpu.tanfovy, cam_cpu.image_height, cam_cpu.image_width,
+                   a.get("shs"), cam_cpu.sh_degree, cam_cpu.campos.numpy())
+    O.backward(st, dl_cpu.numpy())
+    dt = time.perf_counter() - t0
+    return {"value": round(cfg.P / dt / 1e6, 6), "unit": "Msplats/s", "cores": 1, "kind": "port",
+            "sample": f"1 view of the same workload ({cfg.P} Gaussians, {cam_cpu.image_width}x"
+                      f"{cam_cpu.image_height}, SH{cfg.sh_degree}) fwd+bwd by the single-threaded C "
+                      f"oracle (oracle/gsr_oracle.c), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--views-per-rank", type=int, default=1)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import splat_scenes as S
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    _C.load_library()
+
+    base = S.CONFIGS[args.config]
+    cfg = S.SceneConfig(base.name, base.P, base.width, base.height, base.focal, base.s0,
+                        sh_degree=base.sh_degree, views=S.RIG27)
+    params_cpu = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0, device="cpu")
+    params = {k: torch.nn.Parameter(v.to(dev)) for k, v in params_cpu.items()}
+    cams = S.scene_cameras(cfg, device=dev)
+    dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
+    V = args.views_per_rank
+
+    def step(it):
+        for j in range(V):
+            cam = cams[(it * world * V + rank * V + j) % len(cams)]
+            a = S.activated_inputs(params, cfg.sh_degree)
+            if cfg.sh_degree >= 0:
+                a.pop("colors_precomp")
+            img, _radii, _depth = GaussianRasterizer(raster_settings=cam)(**a)
+            img.backward(dl)
+        if dist is not None:
+            grads = [p.grad for p in params.values()]
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            dist.all_reduce(flat)
+            o = 0
+            for g in grads:
+                n = g.numel()
+                g.copy_(flat[o:o + n].view_as(g))
+                o += n
+        for p in params.values():
+            p.grad = None
+
+    for it in range(args.warmup):
+        step(it)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _C.profile_reset()
+    _C.profile_enable(True)
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        step(args.warmup + it)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _C.profile_enable(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel device time inside the timed region (HIP events on the launch stream)
+    phases = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
+              "render_bwd", "gauss_bwd"]
+    times = {ph: _C.profile_read(ph) for ph in phases}
+    # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
+    used = sorted({(it * world * V + rank * V + j) % len(cams)
+                   for it in range(args.warmup, args.warmup + args.steps) for j in range(V)})
+    Ks = []
+    with torch.no_grad():
+        a = S.activated_inputs(params, cfg.sh_degree)
+        if cfg.sh_degree >= 0:
+            a.pop("colors_precomp")
+        e = torch.empty(0, device=dev)
+        colors = a.get("colors_precomp")
+        for ci in used:
+            c = cams[ci]
+            Ks.append(_C.rasterize_gaussians(c.bg, a["means3D"], colors if colors is not None else e,
+                                             a["opacities"], a["scales"], a["rotations"], 1.0, e,
+                                             c.viewmatrix, c.projmatrix, c.tanfovx, c.tanfovy,
+                                             cfg.height, cfg.width, a.get("shs", e), c.sh_degree,
+                                             c.campos, False)[0])
+    K = float(np.mean(Ks))
+    N = cfg.width * cfg.height
+    T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
+    F = 12 * (cfg.sh_degree + 1) ** 2 if cfg.sh_degree >= 0 else 12
+    dom = max(phases, key=lambda ph: times[ph][0])
+    tot_ms, cnt = times[dom]
+    avg_ms = tot_ms / max(cnt, 1)
+    bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, cfg.sh_degree >= 0)
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * V * cfg.P / (elapsed / args.steps) / 1e6
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            yaw, hgt = cfg.views[0]
+            cam_cpu = S.render_settings(cfg.width, cfg.height, S.intrinsics(cfg.focal, cfg.width, cfg.height),
+                                        S.look_at(yaw, hgt, cfg.distance), device="cpu",
+                                        sh_degree=max(cfg.sh_degree, 0))
+            cpu = cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl.cpu())
+        out = {
+            "metric": "Msplats/sec fwd+bwd @1080p (1M gauss)",
+            "value": round(value, 3), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"{cfg.name}: {cfg.P} Gaussians, SH{cfg.sh_degree}, "
+                                   f"{cfg.width}x{cfg.height}, 27-camera rig, {V} view(s)/GPU/step, fwd+bwd",
+                       "gaussians": cfg.P, "views_per_gpu_per_step": V,
+                       "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
+                       "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch)},
+            "phase_ms_per_launch": {ph: round(times[ph][0] / max(times[ph][1], 1), 5) for ph in phases},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * gsr.h -- C ABI of the MI355X-native differentiable Gaussian-splat rasterizer (libgsr.so).
+ *
+ * This is the native boundary under the Python drop-in `diff_gaussian_rasterization`
+ * (GaussianRasterizer / GaussianRasterizationSettings, imported by the reference at
+ * train.py:16, densify.py:9, shared.py:9).  Each entry point replaces one function of the
+ * reference's native extension `diff_gaussian_rasterization._C`, whose source is the (empty here)
+ * submodule `diff-gaussian-rasterization-w-depth` (.gitmodules:1-3); see SURVEY.md section 2.1:
+ *
+ *   gsr_forward       <- _C.rasterize_gaussians           (rasterize_points.cu RasterizeGaussiansCUDA,
+ *                                                          CudaRasterizer::Rasterizer::forward)
+ *   gsr_backward      <- _C.rasterize_gaussians_backward  (RasterizeGaussiansBackwardCUDA,
+ *                                                          CudaRasterizer::Rasterizer::backward)
+ *   gsr_mark_visible  <- _C.mark_visible                  (markVisible)
+ *
+ * Plain pointers and sizes only; no torch types.  All tensor pointers are DEVICE pointers to
+ * contiguous fp32 data in the reference's own layouts (means3D (P,3), shs (P,M,3), colors (P,3),
+ * opacities (P,1), scales (P,3), rotations (P,4) = quaternion (w,x,y,z), cov3D (P,6) upper
+ * triangle).  Matrices are the 16 floats of the `.contiguous()` (1,4,4) tensors built by
+ * shared.py:80,110,120 (column-major: x' = m[0]x + m[4]y + m[8]z + m[12]).
+ *
+ * Every call is asynchronous on `stream` (a hipStream_t; NULL = legacy default stream) except for
+ * the single device->host read of num_rendered inside gsr_forward, which the reference also does.
+ * Functions return GSR_OK (0) or an error code; gsr_last_error() gives the thread-local message.
+ */
+#ifndef GSR_H
+#define GSR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_ABI_VERSION 1
+
+enum gsr_status {
+    GSR_OK = 0,
+    GSR_ERR_ARG = 1,         /* invalid argument (shape/combination); message in gsr_last_error() */
+    GSR_ERR_HIP = 2,         /* HIP runtime / kernel launch error */
+    GSR_ERR_ALLOC = 3,       /* the allocation callback returned NULL */
+    GSR_ERR_UNSUPPORTED = 4  /* configuration outside the supported envelope */
+};
+
+/* Buffer kinds requested through the allocation callback.  They mirror the reference's
+ * geometryBuffer / binningBuffer / imageBuffer resize functors (rasterize_points.cu), plus the
+ * backward pass's transient scratch.  The caller owns every returned buffer; GEOM, BINNING and
+ * IMAGE must be kept alive and handed back to gsr_backward. */
+enum gsr_buffer { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2, GSR_BUF_SCRATCH = 3 };
+
+/* Returns a device pointer of at least `bytes` bytes, 256-byte aligned, or NULL on failure. */
+typedef void *(*gsr_alloc_fn)(void *ctx, int which, size_t bytes);
+
+/* Camera / raster settings: the 11 fields of GaussianRasterizationSettings (shared.py:112-124). */
+typedef struct gsr_camera {
+    int image_width;
+    int image_height;
+    float tan_fovx;          /* = W / (2 fx)  (shared.py:115) */
+    float tan_fovy;          /* = H / (2 fy)  (shared.py:116) */
+    const float *viewmatrix; /* device, 16 floats */
+    const float *projmatrix; /* device, 16 floats (= view * proj, shared.py:120) */
+    const float *campos;     /* device, 3 floats */
+    const float *bg;         /* device, 3 floats */
+    int prefiltered;         /* accepted; the near-plane cull is applied either way */
+} gsr_camera;
+
+/* Per-Gaussian inputs: the render arguments of shared.py:29-42 (already activated). */
+typedef struct gsr_gaussians {
+    int P;                       /* number of Gaussians (>= 0) */
+    int sh_degree;               /* active SH degree D (0..3) */
+    int sh_coeffs;               /* M = shs.size(1), 0 when shs is NULL */
+    float scale_modifier;
+    const float *means3D;        /* (P,3) required */
+    const float *shs;            /* (P,M,3) or NULL -- exactly one of shs / colors_precomp */
+    const float *colors_precomp; /* (P,3)   or NULL */
+    const float *opacities;      /* (P,1) required */
+    const float *scales;         /* (P,3)   or NULL -- scales+rotations, or cov3D_precomp */
+    const float *rotations;      /* (P,4)   or NULL */
+    const float *cov3D_precomp;  /* (P,6)   or NULL */
+} gsr_gaussians;
+
+/* Gradient outputs of gsr_backward, in the order _C.rasterize_gaussians_backward returns them.
+ * Every element of every non-NULL array is written (no pre-zeroing needed). */
+typedef struct gsr_grads {
+    float *dL_dmeans2D;   /* (P,3)  NDC units, z = 0 */
+    float *dL_dcolors;    /* (P,3) */
+    float *dL_dopacity;   /* (P,1) */
+    float *dL_dmeans3D;   /* (P,3) */
+    float *dL_dcov3D;     /* (P,6) */
+    float *dL_dsh;        /* (P,M,3) or NULL when M == 0 */
+    float *dL_dscales;    /* (P,3) */
+    float *dL_drotations; /* (P,4) */
+} gsr_grads;
+
+/* Forward: preprocess -> tile binning -> per-tile depth sort -> alpha blend (colour + depth).
+ * Writes out_color (3,H,W), out_depth (1,H,W), out_radii (P) and *out_num_rendered.  The three
+ * persistent buffers are requested through `alloc` (GEOM, IMAGE, then BINNING once the
+ * Gaussian/tile pair count is known).  P == 0 writes zeros (no background), like the reference. */
+int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                float *out_color, float *out_depth, int *out_radii, int *out_num_rendered,
+                void *stream);
+
+/* Backward of gsr_forward given dL/d(color) (3,H,W).  dL_ddepth is accepted and ignored: the
+ * reference discards the depth output (train.py:355-361, densify.py:120-126) and its -w-depth
+ * backward does not propagate it.  Requests one SCRATCH buffer through `alloc`. */
+int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
+                 const void *geom, const void *binning, const void *image, const float *dL_dcolor,
+                 const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
+                 void *stream);
+
+/* present[i] = Gaussian i passes the near-plane frustum test (view-space z > 0.2). */
+int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,
+                     uint8_t *present, void *stream);
+
+/* Byte sizes of the buffers gsr_forward requests (for callers that pre-allocate pools). */
+size_t gsr_geom_bytes(int P);
+size_t gsr_image_bytes(int width, int height, int P);
+size_t gsr_binning_bytes(int num_rendered);
+size_t gsr_scratch_bytes(int num_rendered);
+
+/* Introspection for parity tests: byte offsets of the arrays inside the three forward buffers, in
+ * this order: geom {depth, xy, conic_op, rgbd, rect, tiles, goff}, image {ranges, final_T,
+ * n_contrib, tile_maxc}, binning {keys, point_list, inv}.  Returns the count written (14). */
+int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *out, int max_out);
+
+const char *gsr_last_error(void);
+int gsr_abi_version(void);
+
+/* Per-phase device timing with HIP events recorded on the call's stream (off by default).
+ * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
+ * "render_bwd", "gauss_bwd".  gsr_profile_read synchronises on the recorded events. */
+int gsr_profile_enable(int on);
+int gsr_profile_reset(void);
+int gsr_profile_read(const char *phase, double *total_ms, int *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H */

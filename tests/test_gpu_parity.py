@@ -1,0 +1,252 @@
+"""GPU parity: the HIP rasterizer (through the C ABI) against the CPU oracle on identical inputs.
+
+Bar (BASELINE.json north_star): tile/bin indices bit-exact -- radii, tiles touched, tile rects,
+tile ranges, sorted Gaussian lists, sort keys, screen-space means/conics/depths; rendered colour,
+depth and every gradient within 1e-4 relative (fp32).  Gradients are summed in a different order
+than the oracle (per-tile wave reductions vs. a serial loop), so they are compared with
+|gpu - oracle| <= 1e-4 |oracle| + 1e-5 max|oracle|.  Blend decisions (alpha >= 1/255,
+T >= 1e-4) can flip when GPU expf and glibc expf differ by an ulp on a pair sitting exactly on a
+threshold; that is allowed for at most 1e-4 of the pixels and reported.
+"""
+import numpy as np
+import pytest
+import torch
+
+import splat_scenes as S
+from diff_gaussian_rasterization import GaussianRasterizer, _C
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4
+
+
+def _inputs(P, W, H, focal, s0, seed=0, sh_degree=-1, yaw=0.0, height=0.0, distance=4.0,
+            bg=(0.0, 0.0, 0.0)):
+    p = S.synthetic_cloud(P, s0, sh_degree=sh_degree, seed=seed, device="cpu")
+    a = {k: (v.detach() if isinstance(v, torch.Tensor) else v)
+         for k, v in S.activated_inputs(p, sh_degree).items()}
+    rs = S.render_settings(W, H, S.intrinsics(focal, W, H), S.look_at(yaw, height, distance),
+                           device="cpu", sh_degree=max(sh_degree, 0))
+    rs = rs._replace(bg=torch.tensor(bg, dtype=torch.float32))
+    return a, rs
+
+
+def _gpu_forward(a, rs, dev, cov3D=None):
+    e = torch.empty(0, device=dev)
+    g = lambda k: a[k].to(dev) if a.get(k) is not None else e  # noqa: E731
+    out = _C.rasterize_gaussians(
+        rs.bg.to(dev), a["means3D"].to(dev), g("colors_precomp"), a["opacities"].to(dev),
+        e if cov3D is not None else g("scales"), e if cov3D is not None else g("rotations"),
+        rs.scale_modifier, cov3D.to(dev) if cov3D is not None else e, rs.viewmatrix.to(dev),
+        rs.projmatrix.to(dev), rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, g("shs"),
+        rs.sh_degree, rs.campos.to(dev), rs.prefiltered)
+    K, color, radii, geom, binning, img, depth = out
+    P = a["means3D"].shape[0]
+    dec = _C.decode_buffers(P, rs.image_width, rs.image_height, K, geom, binning, img)
+    return dict(K=K, color=color, radii=radii, geom=geom, binning=binning, img=img, depth=depth,
+                dec=dec)
+
+
+def _gpu_backward(a, rs, dev, fw, dl, cov3D=None):
+    e = torch.empty(0, device=dev)
+    g = lambda k: a[k].to(dev) if a.get(k) is not None else e  # noqa: E731
+    return _C.rasterize_gaussians_backward(
+        rs.bg.to(dev), a["means3D"].to(dev), fw["radii"], g("colors_precomp"),
+        e if cov3D is not None else g("scales"), e if cov3D is not None else g("rotations"),
+        rs.scale_modifier, cov3D.to(dev) if cov3D is not None else e, rs.viewmatrix.to(dev),
+        rs.projmatrix.to(dev), rs.tanfovx, rs.tanfovy, dl.to(dev), g("shs"), rs.sh_degree,
+        rs.campos.to(dev), fw["geom"], fw["K"], fw["binning"], fw["img"])
+
+
+def _ora_forward(a, rs, cov3D=None):
+    n = lambda k: a[k].numpy() if a.get(k) is not None else None  # noqa: E731
+    return O.forward(rs.bg.numpy(), a["means3D"].numpy(), n("colors_precomp"), a["opacities"].numpy(),
+                     None if cov3D is not None else n("scales"),
+                     None if cov3D is not None else n("rotations"), rs.scale_modifier,
+                     cov3D.numpy() if cov3D is not None else None, rs.viewmatrix, rs.projmatrix,
+                     rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, n("shs"),
+                     rs.sh_degree, rs.campos.numpy())
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _close(name, got, ref, rtol=RTOL, atol_frac=1e-5, max_bad_frac=0.0):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, (name, got.shape, ref.shape)
+    if ref.size == 0:
+        return
+    scale = np.abs(ref).max() + 1e-30
+    bad = np.abs(got - ref) > rtol * np.abs(ref) + atol_frac * scale
+    frac = bad.mean()
+    assert frac <= max_bad_frac, (f"{name}: {bad.sum()}/{bad.size} outside tolerance, worst "
+                                  f"{np.abs(got - ref).max():.3g} (scale {scale:.3g})")
+
+
+def check_forward(fw, st, pix_flip_frac=1e-4):
+    """Bit-exact integer state + tolerance on blended images."""
+    d = fw["dec"]
+    P = st["P"]
+    assert fw["K"] == st["num_rendered"]
+    np.testing.assert_array_equal(_np(fw["radii"]), st["radii"])
+    np.testing.assert_array_equal(_np(d["tiles_touched"]).view(np.uint32), st["tiles_touched"])
+    vis = st["radii"] > 0
+    r = _np(d["rect"]).view(np.uint32)
+    rect = np.stack([r[:, 0] & 0xFFFF, r[:, 0] >> 16, r[:, 1] & 0xFFFF, r[:, 1] >> 16], -1)
+    np.testing.assert_array_equal(rect[vis], st["rects"][vis])
+    np.testing.assert_array_equal(_np(d["depth"])[vis].view(np.uint32), st["depths"][vis].view(np.uint32))
+    np.testing.assert_array_equal(_np(d["xy"])[vis].view(np.uint32), st["xy"][vis].view(np.uint32))
+    np.testing.assert_array_equal(_np(d["conic_opacity"])[vis].view(np.uint32),
+                                  st["conic_opacity"][vis].view(np.uint32))
+    np.testing.assert_array_equal(_np(d["ranges"]).view(np.uint32), st["ranges"])
+    np.testing.assert_array_equal(_np(d["point_list"]).view(np.uint32), st["point_list"])
+    if st["sh"] is not None:
+        _close("rgb", _np(d["rgbd"])[vis, :3], st["rgb"][vis], atol_frac=1e-6)
+    # goff: exclusive emission offsets; inv is a permutation of the slots
+    goff = _np(d["goff"]).astype(np.int64)
+    tt = st["tiles_touched"].astype(np.int64)
+    np.testing.assert_array_equal(goff[:P], np.concatenate([[0], np.cumsum(tt)[:-1]]) if P else goff[:0])
+    assert goff[P] == st["num_rendered"]
+    inv = _np(d["inv"]).astype(np.int64)
+    assert np.array_equal(np.sort(inv), np.arange(st["num_rendered"]))
+    # blended outputs
+    H, W = st["H"], st["W"]
+    same_nc = (_np(d["n_contrib"]).view(np.uint32) == st["n_contrib"]).mean()
+    assert same_nc >= 1 - pix_flip_frac, f"n_contrib differs on {1 - same_nc:.2e} of pixels"
+    _close("final_T", _np(d["final_T"]), st["final_T"], atol_frac=1e-6, max_bad_frac=pix_flip_frac)
+    _close("color", _np(fw["color"]), st["color"], atol_frac=1e-6, max_bad_frac=pix_flip_frac)
+    _close("depth", _np(fw["depth"]), st["depth"], atol_frac=1e-6, max_bad_frac=pix_flip_frac)
+    assert fw["color"].shape == (3, H, W) and fw["depth"].shape == (1, H, W)
+
+
+def check_backward(gb, gref, P, M, grad_flip_frac=1e-3):
+    (dm2, dcol, dop, dm3, dcov, dsh, dsc, drot) = [_np(t) for t in gb]
+    _close("means2D", dm2, gref["means2D"], max_bad_frac=grad_flip_frac)
+    _close("colors", dcol, gref["colors"], max_bad_frac=grad_flip_frac)
+    _close("opacities", dop, gref["opacities"], max_bad_frac=grad_flip_frac)
+    _close("means3D", dm3, gref["means3D"], max_bad_frac=grad_flip_frac)
+    _close("cov3D", dcov, gref["cov3D"], max_bad_frac=grad_flip_frac)
+    _close("scales", dsc, gref["scales"], max_bad_frac=grad_flip_frac)
+    _close("rotations", drot, gref["rotations"], max_bad_frac=grad_flip_frac)
+    assert dsh.shape == (P, M, 3)
+    if M:
+        _close("sh", dsh, gref["sh"], max_bad_frac=grad_flip_frac)
+
+
+CASES = {
+    # name: (P, W, H, focal, s0, sh_degree, extra)
+    "c1": (10_000, 256, 256, 256.0, 0.02, -1, {}),
+    "ragged_bg": (3_000, 200, 120, 150.0, 0.03, -1, dict(bg=(0.2, 0.5, 0.9))),
+    "sh1_yaw": (5_000, 160, 96, 120.0, 0.03, 1, dict(yaw=90.0, height=0.8)),
+    "sh3": (20_000, 480, 270, 400.0, 0.01, 3, {}),
+    "dense_small": (4_000, 64, 48, 64.0, 0.08, -1, {}),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_forward_backward_parity(case, cuda):
+    P, W, H, f, s0, shd, extra = CASES[case]
+    a, rs = _inputs(P, W, H, f, s0, seed=3, sh_degree=shd, **extra)
+    st = _ora_forward(a, rs)
+    fw = _gpu_forward(a, rs, cuda)
+    check_forward(fw, st)
+    dl = S.upstream_grad(H, W, device="cpu")
+    gref = O.backward(st, dl.numpy())
+    gb = _gpu_backward(a, rs, cuda, fw, dl)
+    check_backward(gb, gref, P, st["M"])
+
+
+def test_cov3d_precomp_parity(cuda):
+    a, rs = _inputs(3_000, 128, 96, 96.0, 0.03, seed=5)
+    from oracle import dense_torch as DT
+    cov = DT.cov3d_from(a["scales"].double(), a["rotations"].double(), 1.0).float()
+    st = _ora_forward(a, rs, cov3D=cov)
+    fw = _gpu_forward(a, rs, cuda, cov3D=cov)
+    check_forward(fw, st)
+    dl = S.upstream_grad(96, 128, device="cpu")
+    gref = O.backward(st, dl.numpy())
+    check_backward(_gpu_backward(a, rs, cuda, fw, dl, cov3D=cov), gref, 3_000, 0)
+
+
+def test_depth_ties_follow_index_order(cuda):
+    """Cloned Gaussians (densify clone, external.py:234-239) share depth: order must be by index."""
+    a, rs = _inputs(2_000, 128, 128, 128.0, 0.03, seed=11)
+    for k in ("means3D", "colors_precomp", "opacities", "scales", "rotations"):
+        a[k] = torch.cat([a[k], a[k][:700]], 0)  # 700 exact duplicates appended
+    st = _ora_forward(a, rs)
+    fw = _gpu_forward(a, rs, cuda)
+    check_forward(fw, st)
+
+
+def test_long_tile_lists(cuda):
+    """> 4096 Gaussians in one tile exercises the long-list sort path."""
+    g = torch.Generator().manual_seed(4)
+    P = 12_000
+    m = torch.zeros(P, 3)
+    m[:, 0] = torch.rand(P, generator=g) * 0.02 - 0.01
+    m[:, 1] = torch.rand(P, generator=g) * 0.02 - 0.01
+    m[:, 2] = torch.rand(P, generator=g) * 2 - 1
+    a = {"means3D": m, "colors_precomp": torch.rand(P, 3, generator=g),
+         "opacities": torch.full((P, 1), 0.05), "scales": torch.full((P, 3), 0.004),
+         "rotations": torch.tensor([[1.0, 0, 0, 0]]).repeat(P, 1)}
+    rs = S.render_settings(64, 64, S.intrinsics(64.0, 64, 64), S.look_at(0, 0, 4), device="cpu")
+    st = _ora_forward(a, rs)
+    assert np.diff(st["ranges"].astype(np.int64), axis=1).max() > 4096
+    fw = _gpu_forward(a, rs, cuda)
+    check_forward(fw, st)
+    dl = S.upstream_grad(64, 64, device="cpu")
+    check_backward(_gpu_backward(a, rs, cuda, fw, dl), O.backward(st, dl.numpy()), P, 0)
+
+
+def test_empty_and_all_culled(cuda):
+    rs = S.render_settings(48, 32, S.intrinsics(48.0, 48, 32), S.look_at(0, 0, 4), device="cpu")
+    rs = rs._replace(bg=torch.tensor([0.25, 0.5, 0.75]))
+    z3 = torch.zeros(0, 3)
+    a = {"means3D": z3, "colors_precomp": z3, "opacities": torch.zeros(0, 1), "scales": z3,
+         "rotations": torch.zeros(0, 4)}
+    fw = _gpu_forward(a, rs, cuda)
+    assert fw["K"] == 0 and not fw["color"].any() and not fw["depth"].any()  # P == 0: no background
+    gb = _gpu_backward(a, rs, cuda, fw, torch.ones(3, 32, 48))
+    assert all(t.shape[0] == 0 for t in gb)
+    m = torch.tensor([[0.0, 0.0, -10.0]]).repeat(5, 1)
+    a = {"means3D": m, "colors_precomp": torch.ones(5, 3), "opacities": torch.ones(5, 1),
+         "scales": torch.full((5, 3), 0.1), "rotations": torch.tensor([[1.0, 0, 0, 0]]).repeat(5, 1)}
+    fw = _gpu_forward(a, rs, cuda)
+    assert fw["K"] == 0 and not fw["radii"].any()
+    assert torch.equal(fw["color"].cpu(), rs.bg[:, None, None].expand(3, 32, 48))
+    gb = _gpu_backward(a, rs, cuda, fw, torch.ones(3, 32, 48))
+    assert all(not t.any() for t in gb)
+
+
+def test_rasterizer_module_autograd(cuda):
+    """The drop-in nn.Module + autograd.Function route, as train.py / densify.py call it."""
+    P = 5_000
+    p = S.synthetic_cloud(P, 0.02, seed=9, device=cuda)
+    params = {k: torch.nn.Parameter(v) for k, v in p.items()}
+    rs = S.render_settings(160, 128, S.intrinsics(160.0, 160, 128), S.look_at(30, 0.3, 4), device=cuda)
+    args = S.render_arguments(params)
+    args["means2D"].retain_grad()
+    img, radii, depth = GaussianRasterizer(raster_settings=rs)(**args)
+    assert img.shape == (3, 128, 160) and radii.dtype == torch.int32 and depth.shape == (1, 128, 160)
+    dl = S.upstream_grad(128, 160, device=cuda)
+    (img * dl).sum().backward()
+    # oracle on the same activated inputs
+    a = {k: v.detach().cpu() for k, v in args.items() if k != "means2D"}
+    st = _ora_forward(a, rs._replace(bg=rs.bg.cpu(), viewmatrix=rs.viewmatrix.cpu(),
+                                     projmatrix=rs.projmatrix.cpu(), campos=rs.campos.cpu()))
+    np.testing.assert_array_equal(_np(radii), st["radii"])
+    gref = O.backward(st, dl.cpu().numpy())
+    _close("means2D.grad", _np(args["means2D"].grad), gref["means2D"], max_bad_frac=1e-3)
+    _close("colors.grad", _np(params["colors"].grad), gref["colors"], max_bad_frac=1e-3)
+    assert params["means"].grad is not None and params["log_scales"].grad is not None
+    assert params["rotation_quaternions"].grad is not None and params["opacity_logits"].grad is not None
+    with pytest.raises(Exception):
+        GaussianRasterizer(raster_settings=rs)(means3D=args["means3D"], means2D=args["means2D"],
+                                               opacities=args["opacities"], scales=args["scales"],
+                                               rotations=args["rotations"])
+    vis = GaussianRasterizer(raster_settings=rs).markVisible(params["means"].detach())
+    np.testing.assert_array_equal(_np(vis), O.mark_visible(p["means"].cpu().numpy(), rs.viewmatrix.cpu(),
+                                                           rs.projmatrix.cpu()))
