@@ -9,6 +9,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -46,6 +48,8 @@ std::mutex g_prof_mu;
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
 std::vector<hipEvent_t> g_evpool;
+std::map<std::string, double> g_host_ms;
+std::map<std::string, int> g_host_n;
 
 hipEvent_t ev_get() {
     if (!g_evpool.empty()) { hipEvent_t e = g_evpool.back(); g_evpool.pop_back(); return e; }
@@ -70,12 +74,36 @@ struct Phase {
     }
 };
 
-// pinned host word for the num_rendered read-back (one per thread)
-uint32_t *pinned_word() {
-    thread_local uint32_t *p = nullptr;
-    if (!p && hipHostMalloc((void **)&p, sizeof(uint32_t) * 4, hipHostMallocDefault) != hipSuccess) p = nullptr;
-    return p;
+// Host-mapped, coherent pinned word per thread for the num_rendered read-back.  k_bin_scan stores
+// K into it with a system-scope store; the host spins on it (no copy kernel, no runtime wait).
+struct HostWord { uint32_t *h = nullptr; uint32_t *d = nullptr; };
+HostWord pinned_word() {
+    thread_local HostWord w;
+    if (!w.h) {
+        uint32_t *h = nullptr;
+        if (hipHostMalloc((void **)&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return w;
+        uint32_t *d = nullptr;
+        if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) { (void)hipHostFree(h); return w; }
+        w.h = h; w.d = d;
+    }
+    return w;
 }
+
+constexpr uint32_t kNoValue = 0xFFFFFFFFu;
+
+// host-side timers (profiling mode only)
+using hclock = std::chrono::steady_clock;
+struct HostPhase {
+    const char *name; hclock::time_point t0; bool on;
+    explicit HostPhase(const char *n) : name(n), t0(hclock::now()), on(g_prof_on) {}
+    ~HostPhase() {
+        if (!on) return;
+        const double ms = std::chrono::duration<double, std::milli>(hclock::now() - t0).count();
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_host_ms[name] += ms;
+        g_host_n[name] += 1;
+    }
+};
 
 int check_common(const gsr_camera *cam, const gsr_gaussians *g, bool need_opacity) {
     if (!cam || !g) return fail(GSR_ERR_ARG, "null camera or gaussians");
@@ -115,14 +143,15 @@ void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
 
 void carve_geom(FwdArgs &a, char *base) {
     const GeomLayout L(a.P);
-    a.depth = (float *)(base + L.depth); a.xy = (float2 *)(base + L.xy);
-    a.conic_op = (float4 *)(base + L.conic_op); a.rgbd = (float4 *)(base + L.rgbd);
+    a.depth = (float *)(base + L.depth); a.rec = (float4 *)(base + L.rec);
     a.rect = (uint2 *)(base + L.rect); a.tiles = (uint32_t *)(base + L.tiles); a.goff = (uint32_t *)(base + L.goff);
 }
 void carve_image(FwdArgs &a, char *base) {
     const ImageLayout L(a.W, a.H, a.P);
     a.ranges = (uint2 *)(base + L.ranges); a.final_T = (float *)(base + L.final_T);
     a.n_contrib = (uint32_t *)(base + L.n_contrib); a.tile_maxc = (uint32_t *)(base + L.tile_maxc);
+    a.tile_cost = (uint32_t *)(base + L.tile_cost); a.tile_order_f = (uint32_t *)(base + L.tile_order_f);
+    a.tile_order_b = (uint32_t *)(base + L.tile_order_b);
     a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
     a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
     a.meta = (uint32_t *)(base + L.meta);
@@ -149,17 +178,18 @@ int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const GeomLayout g(P);
     const ImageLayout im(W, H, P);
     const BinningLayout b(K);
-    const size_t v[14] = {g.depth, g.xy, g.conic_op, g.rgbd, g.rect, g.tiles, g.goff,
+    const size_t v[12] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
                           im.ranges, im.final_T, im.n_contrib, im.tile_maxc,
                           b.keys, b.point_list, b.inv};
     int n = 0;
-    for (; n < 14 && n < max_out; ++n) out[n] = v[n];
+    for (; n < 12 && n < max_out; ++n) out[n] = v[n];
     return n;
 }
 
 int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
                 float *out_color, float *out_depth, int *out_radii, int *out_num_rendered,
                 void *stream) {
+    HostPhase host_total("host_forward");
     int rc = check_common(cam, g, true);
     if (rc) return rc;
     if (!alloc || !out_color || !out_depth || !out_num_rendered || (g->P > 0 && !out_radii))
@@ -185,12 +215,30 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     }
     { Phase ph(s, "preprocess"); HIP_TRY(launch_preprocess(a, s)); }
     { Phase ph(s, "bin_count"); HIP_TRY(launch_bin_count(a, s)); }
-    { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, s)); }
-    uint32_t *hw = pinned_word();
-    if (!hw) return fail(GSR_ERR_HIP, "hipHostMalloc failed");
-    HIP_TRY(hipMemcpyAsync(hw, a.meta, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    const uint32_t K = hw[0];
+    HostWord hw = pinned_word();
+    if (!hw.h) return fail(GSR_ERR_HIP, "hipHostMalloc(mapped) failed");
+    __atomic_store_n(hw.h, kNoValue, __ATOMIC_SEQ_CST);
+    { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, hw.d, s)); }
+    uint32_t K;
+    {
+        HostPhase hp("host_wait_K");
+        // Spin on the host-mapped word (the scan is queued behind the caller's earlier work on this
+        // stream, so this can take milliseconds).  Every ~0.5 ms ask the runtime whether the stream
+        // has drained or failed, so a faulted launch cannot leave us spinning.
+        auto last = hclock::now();
+        while ((K = __atomic_load_n(hw.h, __ATOMIC_ACQUIRE)) == kNoValue) {
+            __builtin_ia32_pause();
+            if (hclock::now() - last > std::chrono::microseconds(500)) {
+                last = hclock::now();
+                const hipError_t q = hipStreamQuery(s);
+                if (q == hipErrorNotReady) continue;
+                if (q != hipSuccess) return fail(GSR_ERR_HIP, "stream error while waiting for num_rendered: %s", hipGetErrorString(q));
+                K = __atomic_load_n(hw.h, __ATOMIC_ACQUIRE);
+                if (K == kNoValue) return fail(GSR_ERR_HIP, "num_rendered was not published");
+                break;
+            }
+        }
+    }
     if (K > 0x7FFFFFFFu) return fail(GSR_ERR_UNSUPPORTED, "num_rendered overflow");
     *out_num_rendered = (int)K;
     char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)K).total);
@@ -207,6 +255,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
                  const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
                  void *stream) {
     (void)dL_ddepth;
+    HostPhase host_total("host_backward");
     int rc = check_common(cam, g, false);
     if (rc) return rc;
     if (!out) return fail(GSR_ERR_ARG, "gsr_backward: null grads");
@@ -232,8 +281,9 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.colors_precomp = f.colors_precomp; a.cov3D_precomp = f.cov3D_precomp;
     a.viewmatrix = f.viewmatrix; a.projmatrix = f.projmatrix; a.campos = f.campos; a.bg = f.bg;
     a.radii = radii;
-    a.xy = f.xy; a.conic_op = f.conic_op; a.rgbd = f.rgbd; a.rect = f.rect; a.goff = f.goff;
+    a.rec = f.rec; a.rect = f.rect; a.goff = f.goff;
     a.ranges = f.ranges; a.final_T = f.final_T; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
+    a.tile_cost = f.tile_cost; a.tile_order_b = f.tile_order_b;
     a.point_list = f.point_list; a.inv = f.inv;
     a.dL_dcolor = dL_dcolor;
     a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
@@ -264,6 +314,8 @@ int gsr_profile_enable(int on) {
 
 int gsr_profile_reset(void) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_host_ms.clear();
+    g_host_n.clear();
     for (auto &r : g_prof) { g_evpool.push_back(r.a); g_evpool.push_back(r.b); }
     g_prof.clear();
     return GSR_OK;
@@ -272,6 +324,11 @@ int gsr_profile_reset(void) {
 int gsr_profile_read(const char *phase, double *total_ms, int *count) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     double tot = 0; int n = 0;
+    if (phase && !strncmp(phase, "host_", 5)) {  // host-side wall time of the named section
+        if (total_ms) *total_ms = g_host_ms.count(phase) ? g_host_ms[phase] : 0.0;
+        if (count) *count = g_host_n.count(phase) ? g_host_n[phase] : 0;
+        return GSR_OK;
+    }
     for (auto &r : g_prof) {
         if (phase && r.phase != phase) continue;
         if (hipEventSynchronize(r.b) != hipSuccess) return fail(GSR_ERR_HIP, "hipEventSynchronize failed");

@@ -15,116 +15,151 @@
 
 namespace gsr {
 
-constexpr int kBwdBatch = 128;  // Gaussians staged per LDS batch in the reverse walk
+// Backward dispatch order (one block): tiles by descending sum of n_contrib over their pixels.
+__global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *__restrict__ tile_cost,
+                                                         uint32_t *__restrict__ tile_order) {
+    __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_hist[kOrderBuckets];
+    lpt_order(T, [&](int t) {
+        const uint4 c = reinterpret_cast<const uint4 *>(tile_cost)[t];
+        return c.x + c.y + c.z + c.w;
+    }, tile_order, s_hist, s_red);
+}
 
+// One wave64 per tile, 4 pixels per lane, reverse walk over the tile's list in batches of 64;
+// 4 independent tiles per 256-thread block, dispatched by descending work (tile_order).
+// Per surviving (tile, Gaussian) pair each contributing pixel adds s = dL/dG * G times
+// (dx, dy, dx^2, dx dy, dy^2) plus dL/dopacity and dL/dcolour terms; the lane sums its 4 pixels
+// in registers, the wave folds the 9 sums with permlane swaps + DPP (wave_sum9), and at the end of
+// the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
+// quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour)
+// with the exact conic, storing one 36-byte record per sorted slot (coalesced, no atomics).
 __global__ __launch_bounds__(256) void k_render_bwd(
-    int W, int H, int gx, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list,
-    const float2 *__restrict__ xy, const float4 *__restrict__ conic_op, const float4 *__restrict__ rgbd,
-    const float *__restrict__ bg, const float *__restrict__ final_Ts,
+    int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
+    const uint32_t *__restrict__ point_list,
+    const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
     const float *__restrict__ dL_dpixels, float *__restrict__ partial) {
-    __shared__ float2 s_xy[kBwdBatch];
-    __shared__ float4 s_co[kBwdBatch];
-    __shared__ float4 s_col[kBwdBatch];
-    __shared__ float s_acc[4][kPartial][kBwdBatch];  // per-wave sums, summed in fixed order
-    const int tile = blockIdx.x;
+    __shared__ float4 s_rec[kTilesPerBlock][3][64];
+    __shared__ float s_outs[kTilesPerBlock][64 * kPartial];
+    const int wv = threadIdx.x >> 6;
+    const int t_lin = blockIdx.x * kTilesPerBlock + wv;
+    if (t_lin >= T) return;
+    float4(&s_a)[64] = s_rec[wv][0];
+    float4(&s_b)[64] = s_rec[wv][1];
+    float4(&s_c)[64] = s_rec[wv][2];
+    float *s_out = s_outs[wv];
+    const int tile = (int)tile_order[t_lin];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
     if (n <= 0) return;
     const int tx = tile % gx, ty = tile / gx;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int px = tx * kTileW + (tid & 15), py = ty * kTileH + (tid >> 4);
-    const bool inside = px < W && py < H;
-    const int pid = py * W + px;
-    const float pfx = (float)px, pfy = (float)py;
-    const int maxc = min((int)tile_maxc[tile], n);
-    // slots nobody in this tile reached get zero records
-    for (int p = maxc + tid; p < n; p += blockDim.x) {
+    const int lane = threadIdx.x & 63;
+    const int px = tx * kTileW + (lane & 15);
+    const int py0 = ty * kTileH + (lane >> 4);
+    const float pfx = (float)px;
+    const float tx0 = (float)(tx * kTileW), ty0 = (float)(ty * kTileH);
+    const float tx1 = tx0 + (kTileW - 1), ty1 = ty0 + (kTileH - 1);
+    const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
+    const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
+    for (int p = maxc + lane; p < n; p += 64) {  // slots nobody reached: zero records
         float *dst = partial + (size_t)(rg.x + p) * kPartial;
 #pragma unroll
-        for (int k = 0; k < kPartial; ++k) dst[k] = 0.f;
+        for (int q = 0; q < kPartial; ++q) dst[q] = 0.f;
     }
-    const float ddelx_dx = (float)(0.5 * W), ddely_dy = (float)(0.5 * H);
-    const float T_final = inside ? final_Ts[pid] : 0.f;
-    float T = T_final;
-    const uint32_t last_c = inside ? n_contrib[pid] : 0u;
-    float dp0 = 0.f, dp1 = 0.f, dp2 = 0.f;
-    if (inside) { dp0 = dL_dpixels[pid]; dp1 = dL_dpixels[H * W + pid]; dp2 = dL_dpixels[2 * H * W + pid]; }
-    float bg_dot = 0;
-    bg_dot += bg[0] * dp0; bg_dot += bg[1] * dp1; bg_dot += bg[2] * dp2;
-    float ar0 = 0.f, ar1 = 0.f, ar2 = 0.f;       // accum_rec
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;       // last_color
-    float last_alpha = 0.f;
-
-    for (int end = maxc; end > 0; end -= kBwdBatch) {
-        const int start = end > kBwdBatch ? end - kBwdBatch : 0;
-        const int cnt = end - start;
-        __syncthreads();  // previous batch fully consumed
-        if (tid < cnt) {
-            const uint32_t g = point_list[rg.x + start + tid];
-            s_xy[tid] = xy[g];
-            s_co[tid] = conic_op[g];
-            s_col[tid] = rgbd[g];
-        }
-        for (int k = tid; k < 4 * kPartial * kBwdBatch; k += blockDim.x) (&s_acc[0][0][0])[k] = 0.f;
-        __syncthreads();
-        for (int j = cnt - 1; j >= 0; --j) {
-            const uint32_t p = (uint32_t)(start + j);
-            float v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0, v6 = 0, v7 = 0, v8 = 0;
-            bool contrib = false;
-            if (p < last_c) {
-                const float2 q = s_xy[j];
-                const float dx = q.x - pfx, dy = q.y - pfy;
-                const float4 co = s_co[j];
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power <= 0.0f) {
-                    const float G = expf(power);
-                    const float alpha = fminf(0.99f, co.w * G);
-                    if (alpha >= 1.0f / 255.0f) {
-                        contrib = true;
-                        T = T / (1.f - alpha);
-                        const float dchannel_dcolor = alpha * T;
-                        const float4 c = s_col[j];
-                        float dL_dalpha = 0.0f;
-                        ar0 = last_alpha * lc0 + (1.f - last_alpha) * ar0; lc0 = c.x;
-                        dL_dalpha += (c.x - ar0) * dp0; v6 = dchannel_dcolor * dp0;
-                        ar1 = last_alpha * lc1 + (1.f - last_alpha) * ar1; lc1 = c.y;
-                        dL_dalpha += (c.y - ar1) * dp1; v7 = dchannel_dcolor * dp1;
-                        ar2 = last_alpha * lc2 + (1.f - last_alpha) * ar2; lc2 = c.z;
-                        dL_dalpha += (c.z - ar2) * dp2; v8 = dchannel_dcolor * dp2;
-                        dL_dalpha *= T;
-                        last_alpha = alpha;
-                        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                        const float dL_dG = co.w * dL_dalpha;
-                        const float gdx = G * dx, gdy = G * dy;
-                        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                        const float dG_ddely = -gdy * co.z - gdx * co.y;
-                        v0 = dL_dG * dG_ddelx * ddelx_dx;
-                        v1 = dL_dG * dG_ddely * ddely_dy;
-                        v2 = -0.5f * gdx * dx * dL_dG;
-                        v3 = -0.5f * gdx * dy * dL_dG;
-                        v4 = -0.5f * gdy * dy * dL_dG;
-                        v5 = G * dL_dalpha;
-                    }
-                }
-            }
-            if (__ballot(contrib)) {  // wave-uniform: skip the reduction when no lane contributed
-                v0 = wave_sum_lane63(v0); v1 = wave_sum_lane63(v1); v2 = wave_sum_lane63(v2);
-                v3 = wave_sum_lane63(v3); v4 = wave_sum_lane63(v4); v5 = wave_sum_lane63(v5);
-                v6 = wave_sum_lane63(v6); v7 = wave_sum_lane63(v7); v8 = wave_sum_lane63(v8);
-                if (lane == 63) {
-                    s_acc[wid][0][j] = v0; s_acc[wid][1][j] = v1; s_acc[wid][2][j] = v2;
-                    s_acc[wid][3][j] = v3; s_acc[wid][4][j] = v4; s_acc[wid][5][j] = v5;
-                    s_acc[wid][6][j] = v6; s_acc[wid][7][j] = v7; s_acc[wid][8][j] = v8;
-                }
-            }
-        }
-        __syncthreads();
-        if (tid < cnt) {
-            float *dst = partial + (size_t)(rg.x + start + tid) * kPartial;
+    const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
+    const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+    float Tt[4], tbg[4], dp0[4], dp1[4], dp2[4], ar0[4], ar1[4], ar2[4], lc0[4], lc1[4], lc2[4], la[4];
+    uint32_t lastc[4];
 #pragma unroll
-            for (int k = 0; k < kPartial; ++k)
-                dst[k] = ((s_acc[0][k][tid] + s_acc[1][k][tid]) + s_acc[2][k][tid]) + s_acc[3][k][tid];
+    for (int k = 0; k < 4; ++k) {
+        const int py = py0 + 4 * k;
+        const bool inside = px < W && py < H;
+        const int pid = py * W + px;
+        const float Tf = inside ? final_Ts[pid] : 0.f;
+        Tt[k] = Tf;
+        lastc[k] = inside ? n_contrib[pid] : 0u;
+        dp0[k] = inside ? dL_dpixels[pid] : 0.f;
+        dp1[k] = inside ? dL_dpixels[H * W + pid] : 0.f;
+        dp2[k] = inside ? dL_dpixels[2 * H * W + pid] : 0.f;
+        float bd = 0;
+        bd += bg0 * dp0[k]; bd += bg1 * dp1[k]; bd += bg2 * dp2[k];
+        tbg[k] = -Tf * bd;  // background term of dL/dalpha: -T_final / (1 - alpha) * <bg, dL/dpix>
+        ar0[k] = ar1[k] = ar2[k] = 0.f; lc0[k] = lc1[k] = lc2[k] = 0.f; la[k] = 0.f;
+    }
+    const int row = lane >> 4;
+    const int slot0123 = (row == 0) ? 0 : (row == 1) ? 2 : (row == 2) ? 1 : 3;  // wave_sum9 lane map
+    for (int end = maxc; end > 0; end -= 64) {
+        const int start = end > 64 ? end - 64 : 0;
+        const int cnt = end - start;
+#pragma unroll
+        for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
+        bool live = false;
+        float4 cj = make_float4(0.f, 0.f, 0.f, 0.f);  // exact conic of the Gaussian this lane staged
+        if (lane < cnt) {
+            const uint32_t g = point_list[rg.x + start + lane];
+            const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
+            cj = rec[(size_t)kRecF4 * g + 3];
+            s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
+            live = !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0, tx1, ty1);
+        }
+        uint64_t m = __ballot(live);
+        wave_lds_sync();
+        while (m) {
+            const int j = 63 - __builtin_clzll(m);
+            m &= ~(1ull << j);
+            const uint32_t p = (uint32_t)(start + j);
+            const float4 a = s_a[j], b = s_b[j], c = s_c[j];
+            float v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0, v6 = 0, v7 = 0, v8 = 0;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const Blend e = blend_eval(a, b, pfx, (float)(py0 + 4 * k));
+                if (!(p < lastc[k] && blend_ok(e))) continue;
+                any = true;
+                const float r = __builtin_amdgcn_rcpf(1.f - e.alpha);
+                Tt[k] = Tt[k] * r;
+                const float dch = e.alpha * Tt[k];
+                float dLa = 0.0f;
+                ar0[k] = fmaf(la[k], lc0[k] - ar0[k], ar0[k]); lc0[k] = c.x;
+                dLa = fmaf(c.x - ar0[k], dp0[k], dLa); v6 = fmaf(dch, dp0[k], v6);
+                ar1[k] = fmaf(la[k], lc1[k] - ar1[k], ar1[k]); lc1[k] = c.y;
+                dLa = fmaf(c.y - ar1[k], dp1[k], dLa); v7 = fmaf(dch, dp1[k], v7);
+                ar2[k] = fmaf(la[k], lc2[k] - ar2[k], ar2[k]); lc2[k] = c.z;
+                dLa = fmaf(c.z - ar2[k], dp2[k], dLa); v8 = fmaf(dch, dp2[k], v8);
+                dLa *= Tt[k];
+                la[k] = e.alpha;
+                dLa = fmaf(r, tbg[k], dLa);
+                const float sG = b.y * dLa * e.G;  // dL/dG * G
+                const float t = sG * e.dx, u = sG * e.dy;
+                v0 += t;
+                v1 += u;
+                v2 = fmaf(t, e.dx, v2);
+                v3 = fmaf(t, e.dy, v3);
+                v4 = fmaf(u, e.dy, v4);
+                v5 = fmaf(e.G, dLa, v5);
+            }
+            if (__ballot(any)) {
+                const Sum9 sm = wave_sum9(v0, v1, v2, v3, v4, v5, v6, v7, v8);
+                if ((lane & 15) == 0) {
+                    s_out[j * kPartial + slot0123] = sm.r0123;
+                    s_out[j * kPartial + 4 + slot0123] = sm.r4567;
+                    if (lane == 0) s_out[j * kPartial + 8] = sm.r8;
+                }
+            }
+        }
+        wave_lds_sync();
+        if (lane < cnt) {
+            const float *sm = s_out + lane * kPartial;
+            const float S1 = sm[0], S2 = sm[1];
+            float *dst = partial + (size_t)(rg.x + start + lane) * kPartial;
+            dst[0] = (-cj.x * S1 - cj.y * S2) * half_w;  // dL/dmeans2D.x (NDC)
+            dst[1] = (-cj.y * S1 - cj.z * S2) * half_h;  // dL/dmeans2D.y (NDC)
+            dst[2] = -0.5f * sm[2];                      // dL/dconic.a
+            dst[3] = -0.5f * sm[3];                      // dL/dconic.b (b/2 convention)
+            dst[4] = -0.5f * sm[4];                      // dL/dconic.c
+            dst[5] = sm[5];                              // dL/dopacity
+            dst[6] = sm[6]; dst[7] = sm[7]; dst[8] = sm[8];  // dL/dcolour
         }
     }
 }
@@ -406,9 +441,11 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (a.K == 0) return hipSuccess;
-    k_render_bwd<<<T, kTilePix, 0, s>>>(a.W, a.H, a.gx, a.ranges, a.point_list, a.xy, a.conic_op,
-                                        a.rgbd, a.bg, a.final_T, a.n_contrib, a.tile_maxc,
-                                        a.dL_dcolor, a.partial);
+    k_tile_order_bwd<<<1, 1024, 0, s>>>(T, a.tile_cost, a.tile_order_b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_render_bwd<<<div_up(T, kTilesPerBlock), 64 * kTilesPerBlock, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_b, a.ranges, a.point_list, a.rec, a.bg, a.final_T,
+                                  a.n_contrib, a.tile_maxc, a.dL_dcolor, a.partial);
     return hipGetLastError();
 }
 

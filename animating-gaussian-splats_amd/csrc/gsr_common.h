@@ -23,15 +23,21 @@ __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_
 // ---------------------------------------------------------------------------------------------
 // Workspace layouts.  One allocation per kind; every array starts 256-byte aligned.
 // ---------------------------------------------------------------------------------------------
-// GEOM (per Gaussian, P): SoA arrays written by preprocess, read by binning/render/backward.
+// GEOM (per Gaussian, P): written by preprocess, read by binning/render/backward.
+//   rec: one 64-byte render record per Gaussian, so a (tile, Gaussian) gather touches one line:
+//        [0] = (x, y, A2, B2)        [1] = (C2, opacity, depth, tau2)
+//        [2] = (r, g, b, 0)          [3] = (conic_a, conic_b, conic_c, 0)
+//        power * log2(e) = A2 dx^2 + B2 dx dy + C2 dy^2, i.e. (A2, B2, C2) = -log2(e) (a/2, b, c/2),
+//        so the blend weight is one v_exp_f32; tau2 = 2 log2(255 opacity) bounds the alpha >= 1/255
+//        footprint (culling); [3] keeps the exact conic for gradients and introspection.
+//   depth/rect/tiles/goff: SoA arrays for the binning kernels.
+constexpr int kRecF4 = 4;  // float4 per render record (64 B)
 struct GeomLayout {
-    size_t depth, xy, conic_op, rgbd, rect, tiles, goff, total;
+    size_t depth, rec, rect, tiles, goff, total;
     __host__ __device__ GeomLayout(int P) {
         size_t o = 0;
         depth = o;    o = align256(o + sizeof(float) * P);
-        xy = o;       o = align256(o + sizeof(float2) * P);
-        conic_op = o; o = align256(o + sizeof(float4) * P);
-        rgbd = o;     o = align256(o + sizeof(float4) * P);
+        rec = o;      o = align256(o + sizeof(float4) * kRecF4 * (size_t)P);
         rect = o;     o = align256(o + sizeof(uint2) * P);
         tiles = o;    o = align256(o + sizeof(uint32_t) * P);
         goff = o;     o = align256(o + sizeof(uint32_t) * (P + 1));
@@ -52,8 +58,8 @@ struct BinGrid {
 
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
 struct ImageLayout {
-    size_t ranges, final_T, n_contrib, tile_maxc, tile_count, tile_cursor, block_sums, block_off,
-        meta, total;
+    size_t ranges, final_T, n_contrib, tile_maxc, tile_cost, tile_order_f, tile_order_b, tile_count,
+        tile_cursor, block_sums, block_off, meta, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -62,7 +68,10 @@ struct ImageLayout {
         ranges = o;      o = align256(o + sizeof(uint2) * T);
         final_T = o;     o = align256(o + sizeof(float) * N);
         n_contrib = o;   o = align256(o + sizeof(uint32_t) * N);
-        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * T);
+        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter tile (16x4 px)
+        tile_cost = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter: sum of n_contrib
+        tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
+        tile_order_b = o; o = align256(o + sizeof(uint32_t) * T);    // backward dispatch order (LPT)
         tile_count = o;  o = align256(o + sizeof(uint32_t) * T);
         tile_cursor = o; o = align256(o + sizeof(uint32_t) * T);
         block_sums = o;  o = align256(o + sizeof(uint32_t) * (NB + 1));
@@ -266,6 +275,139 @@ __device__ inline float wave_sum_lane63(float v) {
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xA, 0xF, false)); // row_bcast:15
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xC, 0xF, false)); // row_bcast:31
     return v;
+}
+
+constexpr int kTilesPerBlock = 4;
+#define GSR_LOG2E 1.4426950408889634f
+
+// Blend weight of one (pixel, Gaussian) pair, shared by the forward and backward kernels so that
+// both take identical decisions: power2 = power * log2(e) evaluated with FMAs, G = 2^power2.
+struct Blend { float dx, dy, p2, G, alpha; };
+__device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
+    Blend e;
+    e.dx = r0.x - pfx;
+    e.dy = r0.y - pfy;
+    e.p2 = fmaf(e.dx, fmaf(r0.z, e.dx, r0.w * e.dy), r1.x * e.dy * e.dy);
+    e.G = __builtin_amdgcn_exp2f(e.p2);
+    e.alpha = fminf(0.99f, r1.y * e.G);
+    return e;
+}
+__device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }  // render kernels: 4 independent tiles (one wave64 each) per block
+
+// Make this wave's LDS writes visible to its own later LDS reads (waves of a render block work
+// on different tiles and never synchronise with each other).
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Longest-processing-time-first dispatch order, computed by ONE block: order[] lists the T tiles
+// by descending cost(t) (bucketed into 2048 log-free linear buckets; arbitrary order inside a bucket,
+// which only affects scheduling).  `s_hist` must hold 2048 words, `s_red` 16.  All threads call it.
+constexpr int kOrderBuckets = 2048;
+template <typename CostFn>
+__device__ inline void lpt_order(int T, CostFn cost, uint32_t *__restrict__ order, uint32_t *s_hist,
+                                 uint32_t *s_red) {
+    uint32_t mx = 0;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) mx = max(mx, cost(t));
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = mx;
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
+    __syncthreads();
+    mx = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mx = max(mx, s_red[w]);
+    int shift = 0;
+    while ((mx >> shift) >= (uint32_t)kOrderBuckets) ++shift;
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+        atomicAdd(&s_hist[kOrderBuckets - 1 - (cost(t) >> shift)], 1u);  // descending cost
+    __syncthreads();
+    uint32_t carry = 0;
+    for (int base = 0; base < kOrderBuckets; base += blockDim.x) {
+        const int b = base + threadIdx.x;
+        const uint32_t c = b < kOrderBuckets ? s_hist[b] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32(c, s_red, &tot) + carry;
+        if (b < kOrderBuckets) s_hist[b] = ex;
+        carry += tot;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+        order[atomicAdd(&s_hist[kOrderBuckets - 1 - (cost(t) >> shift)], 1u)] = (uint32_t)t;
+}
+
+// XCD-aware bijection over T tiles: blocks b, b+8, ... (one XCD under round-robin dispatch) take a
+// contiguous run of tiles, so neighbouring tiles share Gaussian records in one L2.  Speed only.
+__device__ inline int remap_tile(int b, int T) {
+    const int x = b & 7, i = b >> 3, q = T >> 3, r = T & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
+// Conservative (tile, Gaussian) cull: true only if NO pixel centre of the pixel rectangle
+// [x0, x1] x [y0, y1] can reach alpha >= 1/255.  Q(d) = a dx^2 + 2 b dx dy + c dy^2 is the
+// Mahalanobis form of the blend's power (power = -Q/2); its minimum over the tile rectangle is
+// compared with tau = 2 ln(255 o) with a margin that dominates the fp32 rounding of the per-pixel
+// evaluation (valid while |b| / sqrt(ac) < 0.999; thinner ellipses are never culled).  Culling a
+// pair therefore changes no output: the per-pixel test would have skipped it everywhere.
+__device__ inline bool tile_cull(float gx, float gy, float a, float b, float c, float o, float tau,
+                                 float x0, float y0, float x1, float y1) {
+    if (o < 1.0f / 255.0f) return true;  // alpha = min(.99, o exp(power)) <= o for power <= 0
+    if (!(b * b < 0.998f * a * c)) return false;
+    const float dxlo = gx - x1, dxhi = gx - x0;
+    const float dylo = gy - y1, dyhi = gy - y0;
+    if (dxlo <= 0.f && dxhi >= 0.f && dylo <= 0.f && dyhi >= 0.f) return false;  // centre inside
+    float qmin;
+    {   // edges with dx fixed: minimise over dy
+        float dx = dxlo;
+        float dy = fminf(fmaxf(-b * dx / c, dylo), dyhi);
+        qmin = a * dx * dx + 2.f * b * dx * dy + c * dy * dy;
+        dx = dxhi;
+        dy = fminf(fmaxf(-b * dx / c, dylo), dyhi);
+        qmin = fminf(qmin, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+        // edges with dy fixed: minimise over dx
+        dy = dylo;
+        dx = fminf(fmaxf(-b * dy / a, dxlo), dxhi);
+        qmin = fminf(qmin, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+        dy = dyhi;
+        dx = fminf(fmaxf(-b * dy / a, dxlo), dxhi);
+        qmin = fminf(qmin, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
+    }
+    return qmin > tau * 1.001f + 1e-3f;
+}
+
+// ---- cross-lane sum of 9 values over a wave64 (gfx950) -------------------------------------
+// Folds pairs of values across lane halves with v_permlane32_swap, across rows with
+// v_permlane16_swap, then reduces each 16-lane row with DPP.  Totals end up in:
+//   r0123: lane 0 -> v0, lane 16 -> v2, lane 32 -> v1, lane 48 -> v3
+//   r4567: lane 0 -> v4, lane 16 -> v6, lane 32 -> v5, lane 48 -> v7
+//   r8   : lane 0 -> v8
+// (every lane of a row holds its row's total).  Fixed tree: bitwise reproducible.
+__device__ inline float fold32(float a, float b) {  // lanes 0-31: a folded, lanes 32-63: b folded
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float fold16(float a, float b) {  // rows (a0+a1, b0+b1, a2+a3, b2+b3)
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ inline float row_sum16(float v) {  // every lane of each 16-lane row gets the row sum
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+    return v;
+}
+struct Sum9 { float r0123, r4567, r8; };
+__device__ inline Sum9 wave_sum9(float v0, float v1, float v2, float v3, float v4, float v5, float v6,
+                                 float v7, float v8) {
+    const float p01 = fold32(v0, v1), p23 = fold32(v2, v3), p45 = fold32(v4, v5), p67 = fold32(v6, v7);
+    const float p8 = fold32(v8, 0.f);
+    Sum9 s;
+    s.r0123 = row_sum16(fold16(p01, p23));
+    s.r4567 = row_sum16(fold16(p45, p67));
+    s.r8 = row_sum16(fold16(p8, 0.f));
+    return s;
 }
 
 }  // namespace gsr

@@ -28,9 +28,8 @@ __global__ __launch_bounds__(256) void k_preprocess(
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
     const float *__restrict__ projmatrix, const float *__restrict__ campos, int W, int H,
     float tan_fovx, float tan_fovy, float focal_x, float focal_y, int gx, int gy,
-    int *__restrict__ radii, float *__restrict__ depth_out, float2 *__restrict__ xy_out,
-    float4 *__restrict__ conic_op_out, float4 *__restrict__ rgbd_out, uint2 *__restrict__ rect_out,
-    uint32_t *__restrict__ tiles_out) {
+    int *__restrict__ radii, float *__restrict__ depth_out, float4 *__restrict__ rec_out,
+    uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     // matrices are tiny and uniform: every lane reads the same words (scalar loads)
@@ -77,9 +76,14 @@ __global__ __launch_bounds__(256) void k_preprocess(
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
-    xy_out[i] = make_float2(pix_x, pix_y);
-    conic_op_out[i] = make_float4(cv.z * det_inv, -cv.y * det_inv, cv.x * det_inv, opacities[i]);
-    rgbd_out[i] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);
+    const float o = opacities[i];
+    const float ca = cv.z * det_inv, cb = -cv.y * det_inv, cc = cv.x * det_inv;
+    const float tau2 = o >= 1.0f / 255.0f ? 2.f * log2f(255.f * o) : -1.f;
+    float4 *r = rec_out + (size_t)kRecF4 * i;
+    r[0] = make_float4(pix_x, pix_y, -0.5f * GSR_LOG2E * ca, -GSR_LOG2E * cb);
+    r[1] = make_float4(-0.5f * GSR_LOG2E * cc, o, pv.z, tau2);
+    r[2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+    r[3] = make_float4(ca, cb, cc, 0.f);
     rect_out[i] = pack_rect(x0, y0, x1, y1);
     tiles_out[i] = (uint32_t)((y1 - y0) * (x1 - x0));
 }
@@ -134,8 +138,11 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
                                                    uint32_t *__restrict__ tile_cursor,
                                                    const uint32_t *__restrict__ block_sums,
                                                    uint32_t *__restrict__ block_off,
-                                                   uint32_t *__restrict__ meta) {
+                                                   uint32_t *__restrict__ meta,
+                                                   uint32_t *host_K,
+                                                   uint32_t *__restrict__ tile_order) {
     __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_hist[kOrderBuckets];
     uint32_t carry = 0;
     for (int base = 0; base < T; base += blockDim.x) {
         const int t = base + threadIdx.x;
@@ -157,7 +164,14 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
         if (b < NB) block_off[b] = ex;
         carry2 += tot;
     }
-    if (threadIdx.x == 0) meta[0] = carry;
+    if (threadIdx.x == 0) {
+        meta[0] = carry;
+        // publish K straight into host-mapped pinned memory: the host spins on this word instead of
+        // paying a copy kernel + stream synchronisation (system-scope store, seen by the CPU)
+        if (host_K) __hip_atomic_store(host_K, carry, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // forward render dispatch order: longest tile lists first
+    lpt_order(T, [&](int t) { return tile_count[t]; }, tile_order, s_hist, s_red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -295,73 +309,85 @@ __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restri
 }
 
 // ------------------------------------------------------------------------------------------
-// Front-to-back blend, one 16x16 tile per 256-thread block (4 wave64: each wave = 4 pixel rows).
-// Gaussians are staged through LDS in batches of 256: xy, conic+opacity, rgb+depth (40 B each).
+// Front-to-back blend.  One 256-thread block per 16x16 tile; wave w owns pixel rows 4w..4w+3 (one
+// pixel per lane) and walks the tile's list on its own: wave-private LDS staging, no block
+// barriers, early exit per 64 pixels.  Tiles are dispatched longest list first (tile_order).
+// Gaussians are staged one per lane in batches of 64 (one gather of the 64-byte render record) and
+// a conservative ellipse test against the wave's 16x4 pixel rectangle drops pairs that cannot reach
+// alpha >= 1/255 there; the per-pixel update is branch-free (selects + FMAs).
 __global__ __launch_bounds__(256) void k_render_fwd(
-    int W, int H, int gx, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list,
-    const float2 *__restrict__ xy, const float4 *__restrict__ conic_op, const float4 *__restrict__ rgbd,
-    const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
-    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc) {
-    __shared__ float2 s_xy[kTilePix];
-    __shared__ float4 s_co[kTilePix];
-    __shared__ float4 s_cd[kTilePix];
-    __shared__ uint32_t s_max;
-    const int tile = blockIdx.x;
+    int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
+    const uint32_t *__restrict__ point_list, const float4 *__restrict__ rec, const float *__restrict__ bg,
+    float *__restrict__ out_color, float *__restrict__ out_depth, float *__restrict__ final_T,
+    uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc, uint32_t *__restrict__ tile_cost) {
+    __shared__ float4 s_rec[kTilesPerBlock][3][64];
+    const int wv = threadIdx.x >> 6;
+    float4(&s_a)[64] = s_rec[wv][0];
+    float4(&s_b)[64] = s_rec[wv][1];
+    float4(&s_c)[64] = s_rec[wv][2];
+    const int tile = (int)tile_order[blockIdx.x];
     const int tx = tile % gx, ty = tile / gx;
-    const int tid = threadIdx.x;
-    const int px = tx * kTileW + (tid & 15), py = ty * kTileH + (tid >> 4);
-    const bool inside = px < W && py < H;
+    const int lane = threadIdx.x & 63;
+    const int px = tx * kTileW + (lane & 15);
+    const int py = ty * kTileH + 4 * wv + (lane >> 4);
     const float pfx = (float)px, pfy = (float)py;
+    const float rx0 = (float)(tx * kTileW), ry0 = (float)(ty * kTileH + 4 * wv);
+    const float rx1 = rx0 + (kTileW - 1), ry1 = ry0 + 3;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (tid == 0) s_max = 0;
+    const bool inside = px < W && py < H;
     bool done = !inside;
-    float T = 1.0f, C0 = 0, C1 = 0, C2 = 0, Dp = 0;
-    uint32_t contributor = 0, last = 0;
-    for (int base = 0; base < n; base += kTilePix) {
-        if (__syncthreads_count(done) == kTilePix) break;
-        const int idx = base + tid;
+    float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+    uint32_t last = 0;
+    for (int base = 0; base < n; base += 64) {
+        if (!__ballot(!done)) break;
+        const int idx = base + lane;
+        bool live = false;
         if (idx < n) {
             const uint32_t g = point_list[rg.x + idx];
-            s_xy[tid] = xy[g];
-            s_co[tid] = conic_op[g];
-            s_cd[tid] = rgbd[g];
+            const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
+            s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
+            live = !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, rx0, ry0, rx1, ry1);
         }
-        __syncthreads();
-        const int cnt = min(kTilePix, n - base);
-        for (int j = 0; !done && j < cnt; ++j) {
-            ++contributor;
-            const float2 q = s_xy[j];
-            const float dx = q.x - pfx, dy = q.y - pfy;
-            const float4 co = s_co[j];
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, co.w * expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1 - alpha);
-            if (test_T < 0.0001f) { done = true; continue; }
-            const float4 cd = s_cd[j];
-            C0 += cd.x * alpha * T;
-            C1 += cd.y * alpha * T;
-            C2 += cd.z * alpha * T;
-            Dp += cd.w * alpha * T;
-            T = test_T;
-            last = contributor;
+        uint64_t m = __ballot(live);
+        wave_lds_sync();
+        while (m) {
+            if (!__ballot(!done)) break;
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const float4 a = s_a[j], b = s_b[j], c = s_c[j];
+            const Blend e = blend_eval(a, b, pfx, pfy);
+            const bool ok = !done && blend_ok(e);
+            const float test_T = Tt * (1.f - e.alpha);
+            const bool fin = ok && test_T < 0.0001f;
+            const bool use = ok && !fin;
+            done = done || fin;
+            const float w = use ? e.alpha * Tt : 0.f;
+            C0 = fmaf(c.x, w, C0);
+            C1 = fmaf(c.y, w, C1);
+            C2 = fmaf(c.z, w, C2);
+            Dp = fmaf(b.z, w, Dp);
+            Tt = use ? test_T : Tt;
+            last = use ? (uint32_t)(base + j + 1) : last;
         }
+        wave_lds_sync();
     }
     if (inside) {
         const int pid = py * W + px;
-        final_T[pid] = T;
+        final_T[pid] = Tt;
         n_contrib[pid] = last;
-        out_color[pid] = C0 + T * bg[0];
-        out_color[H * W + pid] = C1 + T * bg[1];
-        out_color[2 * H * W + pid] = C2 + T * bg[2];
+        out_color[pid] = C0 + Tt * bg[0];
+        out_color[H * W + pid] = C1 + Tt * bg[1];
+        out_color[2 * H * W + pid] = C2 + Tt * bg[2];
         out_depth[pid] = Dp;
     }
-    __syncthreads();
-    if (last) atomicMax(&s_max, last);
-    __syncthreads();
-    if (tid == 0) tile_maxc[tile] = s_max;
+    uint32_t mx = last, sum = last;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+        sum += (uint32_t)__shfl_xor((int)sum, d, 64);
+    }
+    if (lane == 0) { tile_maxc[4 * tile + wv] = mx; tile_cost[4 * tile + wv] = sum; }
 }
 
 __global__ void k_zero_f32(float *p, size_t n) {
@@ -388,8 +414,7 @@ hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {
     k_preprocess<<<div_up(a.P, 256), 256, 0, s>>>(
         a.P, a.D, a.M, a.means3D, a.scales, a.scale_modifier, a.rotations, a.opacities, a.shs,
         a.colors_precomp, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
-        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.xy, a.conic_op, a.rgbd,
-        a.rect, a.tiles);
+        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles);
     return hipGetLastError();
 }
 
@@ -406,10 +431,10 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_bin_scan(const FwdArgs &a, hipStream_t s) {
+hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_K, hipStream_t s) {
     const BinGrid bg(a.P);
     k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
-                                  a.block_sums, a.block_off, a.meta);
+                                  a.block_sums, a.block_off, a.meta, host_K, a.tile_order_f);
     return hipGetLastError();
 }
 
@@ -433,9 +458,9 @@ hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s) {
 
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
-    k_render_fwd<<<T, kTilePix, 0, s>>>(a.W, a.H, a.gx, a.ranges, a.point_list, a.xy, a.conic_op,
-                                        a.rgbd, a.bg, a.out_color, a.out_depth, a.final_T,
-                                        a.n_contrib, a.tile_maxc);
+    k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.point_list, a.rec,
+                                   a.bg, a.out_color, a.out_depth, a.final_T, a.n_contrib,
+                                   a.tile_maxc, a.tile_cost);
     return hipGetLastError();
 }
 

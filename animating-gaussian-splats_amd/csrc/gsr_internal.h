@@ -16,9 +16,10 @@ struct FwdArgs {
     const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;
     // geom
-    float *depth; float2 *xy; float4 *conic_op; float4 *rgbd; uint2 *rect; uint32_t *tiles; uint32_t *goff;
+    float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff;
     // image
-    uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc; uint32_t *tile_count;
+    uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc; uint32_t *tile_cost;
+    uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
     // binning
     uint64_t *keys; uint32_t *point_list; uint32_t *inv;
@@ -33,9 +34,10 @@ struct BwdArgs {
     const float *viewmatrix, *projmatrix, *campos, *bg;
     const int *radii;
     // saved state
-    const float2 *xy; const float4 *conic_op; const float4 *rgbd; const uint2 *rect;
+    const float4 *rec; const uint2 *rect;
     const uint32_t *goff; const uint2 *ranges; const float *final_T; const uint32_t *n_contrib;
-    const uint32_t *tile_maxc; const uint32_t *point_list; const uint32_t *inv;
+    const uint32_t *tile_maxc; const uint32_t *tile_cost; uint32_t *tile_order_b;
+    const uint32_t *point_list; const uint32_t *inv;
     // scratch
     float *partial;
     // upstream gradient
@@ -47,7 +49,7 @@ struct BwdArgs {
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);
 hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s);
-hipError_t launch_bin_scan(const FwdArgs &a, hipStream_t s);
+hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_K, hipStream_t s);
 hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s);
 hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s);
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s);

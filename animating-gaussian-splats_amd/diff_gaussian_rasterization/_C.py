@@ -244,8 +244,8 @@ def profile_read(phase=None):
 def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
     """Typed views of the arrays inside the forward buffers (for parity tests / debugging)."""
     L = load_library()
-    offs = (ctypes.c_size_t * 14)()
-    L.gsr_buffer_offsets(int(P), int(W), int(H), int(num_rendered), offs, 14)
+    offs = (ctypes.c_size_t * 12)()
+    L.gsr_buffer_offsets(int(P), int(W), int(H), int(num_rendered), offs, 12)
     o = list(offs)
     T = ((W + 15) // 16) * ((H + 15) // 16)
     K = int(num_rendered)
@@ -255,19 +255,22 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
         return buf[off:off + nbytes].view(dtype).reshape(shape)
 
     f32, i32, i64 = torch.float32, torch.int32, torch.int64
+    rec = view(geomBuffer, o[1], 16 * P, f32, (P, 16))  # 64-byte render records
     return {
         "depth": view(geomBuffer, o[0], P, f32, (P,)),
-        "xy": view(geomBuffer, o[1], 2 * P, f32, (P, 2)),
-        "conic_opacity": view(geomBuffer, o[2], 4 * P, f32, (P, 4)),
-        "rgbd": view(geomBuffer, o[3], 4 * P, f32, (P, 4)),
-        "rect": view(geomBuffer, o[4], 2 * P, i32, (P, 2)),
-        "tiles_touched": view(geomBuffer, o[5], P, i32, (P,)),
-        "goff": view(geomBuffer, o[6], P + 1, i32, (P + 1,)),
-        "ranges": view(imgBuffer, o[7], 2 * T, i32, (T, 2)),
-        "final_T": view(imgBuffer, o[8], W * H, f32, (H, W)),
-        "n_contrib": view(imgBuffer, o[9], W * H, i32, (H, W)),
-        "tile_maxc": view(imgBuffer, o[10], T, i32, (T,)),
-        "keys": view(binningBuffer, o[11], K, i64, (K,)),
-        "point_list": view(binningBuffer, o[12], K, i32, (K,)),
-        "inv": view(binningBuffer, o[13], K, i32, (K,)),
+        "rec": rec,
+        "xy": rec[:, 0:2],
+        "conic_opacity": torch.stack([rec[:, 12], rec[:, 13], rec[:, 14], rec[:, 5]], 1),
+        "rgbd": torch.cat([rec[:, 8:11], rec[:, 6:7]], 1),
+        "tau2": rec[:, 7],
+        "rect": view(geomBuffer, o[2], 2 * P, i32, (P, 2)),
+        "tiles_touched": view(geomBuffer, o[3], P, i32, (P,)),
+        "goff": view(geomBuffer, o[4], P + 1, i32, (P + 1,)),
+        "ranges": view(imgBuffer, o[5], 2 * T, i32, (T, 2)),
+        "final_T": view(imgBuffer, o[6], W * H, f32, (H, W)),
+        "n_contrib": view(imgBuffer, o[7], W * H, i32, (H, W)),
+        "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
+        "keys": view(binningBuffer, o[9], K, i64, (K,)),
+        "point_list": view(binningBuffer, o[10], K, i32, (K,)),
+        "inv": view(binningBuffer, o[11], K, i32, (K,)),
     }

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Profile bench.py with rocprofv3 on the GPU box: kernel trace + stats, then the HBM counters in
+# two separate PMC passes (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950).
+# usage (on the box, from the repo root): bash tools/profile_round.sh <tag> [bench args...]
+set -u
+tag=${1:-r01}; shift || true
+R=$(pwd)
+O=$R/gpurun_out/prof_$tag
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -- \
+    python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline "$@" > "$O/trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
+echo "trace ok"
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/fetch" -- \
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$O/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 2; }
+echo "fetch ok"
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/write" -- \
+    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 3; }
+echo "write ok"

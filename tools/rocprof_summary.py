@@ -1,0 +1,80 @@
+"""Summarise rocprofv3 CSV output into per-kernel tables (profiles/ evidence for bench.py).
+
+Usage:
+  python tools/rocprof_summary.py trace  <dir>            -> per-kernel calls / avg / total us
+  python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> [--out profiles/x.json]
+        -> per-kernel avg FETCH_SIZE / WRITE_SIZE per launch and corrected HBM bytes
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KiB) reports exactly half the
+bytes of a wide coalesced streaming read, so HBM read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is
+exact for 16-B-per-lane streaming stores.  Other access widths are uncalibrated; the corrected
+figure is an estimate and ratios between kernels/variants are what it is trusted for.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def _short(name):
+    m = re.search(r"gsr::(\w+?)(?:<|\(|$)", name) or re.search(r"(k_\w+)", name)
+    return m.group(1) if m else name.split("(")[0][:60]
+
+
+def _rows(d, pattern):
+    files = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    for f in files:
+        with open(f, newline="") as fh:
+            yield from csv.DictReader(fh)
+
+
+def trace(d):
+    acc = defaultdict(list)
+    for r in _rows(d, "*kernel_trace.csv"):
+        acc[_short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = {k: {"calls": len(v), "avg_us": sum(v) / len(v), "total_us": sum(v)} for k, v in acc.items()}
+    return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_us"]))
+
+
+def pmc(fetch_dir, write_dir):
+    res = defaultdict(dict)
+    for d, ctr in ((fetch_dir, "FETCH_SIZE"), (write_dir, "WRITE_SIZE")):
+        acc = defaultdict(list)
+        for r in _rows(d, "*counter_collection.csv"):
+            if r.get("Counter_Name") != ctr:
+                continue
+            acc[_short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        for k, v in acc.items():
+            res[k][ctr + "_KiB_avg"] = sum(v) / len(v)
+            res[k]["launches_" + ctr] = len(v)
+    for k, v in res.items():
+        f = v.get("FETCH_SIZE_KiB_avg", 0.0)
+        w = v.get("WRITE_SIZE_KiB_avg", 0.0)
+        v["hbm_bytes_per_launch_corrected"] = 2 * f * 1024 + w * 1024
+    return dict(res)
+
+
+def main():
+    mode = sys.argv[1]
+    if mode == "trace":
+        t = trace(sys.argv[2])
+        print(f"{'kernel':<28}{'calls':>8}{'avg_us':>12}{'total_us':>14}")
+        for k, v in t.items():
+            print(f"{k:<28}{v['calls']:>8}{v['avg_us']:>12.2f}{v['total_us']:>14.1f}")
+        if "--out" in sys.argv:
+            json.dump(t, open(sys.argv[sys.argv.index("--out") + 1], "w"), indent=1)
+    elif mode == "pmc":
+        p = pmc(sys.argv[2], sys.argv[3])
+        print(f"{'kernel':<28}{'FETCH KiB':>14}{'WRITE KiB':>14}{'HBM MB (corr)':>16}")
+        for k, v in sorted(p.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch_corrected"]):
+            print(f"{k:<28}{v.get('FETCH_SIZE_KiB_avg', 0):>14.1f}{v.get('WRITE_SIZE_KiB_avg', 0):>14.1f}"
+                  f"{v['hbm_bytes_per_launch_corrected'] / 1e6:>16.2f}")
+        if "--out" in sys.argv:
+            json.dump(p, open(sys.argv[sys.argv.index("--out") + 1], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
