@@ -291,7 +291,9 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
     char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, ScratchLayout(num_rendered).total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
-    a.partial = (float *)scr;
+    const ScratchLayout SL(num_rendered);
+    a.part8 = (float4 *)(scr + SL.part8);
+    a.part1 = (float *)(scr + SL.part1);
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
     { Phase ph(s, "gauss_bwd"); HIP_TRY(launch_gauss_bwd(a, s)); }
     return GSR_OK;

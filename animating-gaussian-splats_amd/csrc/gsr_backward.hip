@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const uint32_t *__restrict__ point_list,
     const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
-    const float *__restrict__ dL_dpixels, float *__restrict__ partial) {
+    const float *__restrict__ dL_dpixels, float4 *__restrict__ part8, float *__restrict__ part1) {
     __shared__ float4 s_rec[kTilesPerBlock][3][64];
     __shared__ float s_outs[kTilesPerBlock][64 * kPartial];
     const int wv = threadIdx.x >> 6;
@@ -63,9 +63,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
     const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
     for (int p = maxc + lane; p < n; p += 64) {  // slots nobody reached: zero records
-        float *dst = partial + (size_t)(rg.x + p) * kPartial;
-#pragma unroll
-        for (int q = 0; q < kPartial; ++q) dst[q] = 0.f;
+        const size_t sl = rg.x + p;
+        part8[2 * sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+        part8[2 * sl + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        part1[sl] = 0.f;
     }
     const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
@@ -152,14 +153,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         if (lane < cnt) {
             const float *sm = s_out + lane * kPartial;
             const float S1 = sm[0], S2 = sm[1];
-            float *dst = partial + (size_t)(rg.x + start + lane) * kPartial;
-            dst[0] = (-cj.x * S1 - cj.y * S2) * half_w;  // dL/dmeans2D.x (NDC)
-            dst[1] = (-cj.y * S1 - cj.z * S2) * half_h;  // dL/dmeans2D.y (NDC)
-            dst[2] = -0.5f * sm[2];                      // dL/dconic.a
-            dst[3] = -0.5f * sm[3];                      // dL/dconic.b (b/2 convention)
-            dst[4] = -0.5f * sm[4];                      // dL/dconic.c
-            dst[5] = sm[5];                              // dL/dopacity
-            dst[6] = sm[6]; dst[7] = sm[7]; dst[8] = sm[8];  // dL/dcolour
+            const size_t sl = rg.x + start + lane;
+            part8[2 * sl] = make_float4((-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
+                                        (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
+                                        -0.5f * sm[2],                       // dL/dconic.a
+                                        -0.5f * sm[3]);                      // dL/dconic.b (b/2 convention)
+            part8[2 * sl + 1] = make_float4(-0.5f * sm[4], sm[5], sm[6], sm[7]);  // dconic.c, dopacity, dcolour.rg
+            part1[sl] = sm[8];                                                    // dcolour.b
         }
     }
 }
@@ -173,36 +173,29 @@ __device__ inline float3 dnormvdv(float3 v, float3 dv) {
                        (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
 }
 
-// SH backward; writes all M coefficient rows of dL_dsh (zeros past the active degree).
-__device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *campos,
-                                     const float *__restrict__ sh, const bool *clamped,
-                                     float3 dL_dcolor, float *__restrict__ dL_dsh) {
+// SH backward; writes all M coefficient rows of dL_dsh (zeros past the active degree).  `sh` and
+// `dL_dsh` may alias (the same LDS row): phase 1 reads the coefficients (direction derivative),
+// phase 2 writes the coefficient gradients, which depend only on the direction and dL/dRGB.
+template <typename ShPtr, typename OutPtr>
+__device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *campos, ShPtr sh,
+                                     const bool *clamped, float3 dL_dcolor, OutPtr dL_dsh) {
     const float3 d0 = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
     const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
     const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
     const float dRGB[3] = {dL_dcolor.x * (clamped[0] ? 0.f : 1.f), dL_dcolor.y * (clamped[1] ? 0.f : 1.f),
                            dL_dcolor.z * (clamped[2] ? 0.f : 1.f)};
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
     float dx[3] = {0, 0, 0}, dy[3] = {0, 0, 0}, dz[3] = {0, 0, 0};
-    for (int k = 0; k < M * 3; ++k) dL_dsh[k] = 0.f;
 #define SH(i, c) sh[(i) * 3 + (c)]
-#define DSH(i, c) dL_dsh[(i) * 3 + (c)]
-#pragma unroll
-    for (int c = 0; c < 3; ++c) DSH(0, c) = GSR_SH_C0 * dRGB[c];
+    // ---- phase 1: d(RGB)/d(direction) from the coefficients ----
     if (deg > 0) {
-        const float d1 = -GSR_SH_C1 * y, d2 = GSR_SH_C1 * z, d3 = -GSR_SH_C1 * x;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            DSH(1, c) = d1 * dRGB[c]; DSH(2, c) = d2 * dRGB[c]; DSH(3, c) = d3 * dRGB[c];
             dx[c] = -GSR_SH_C1 * SH(3, c); dy[c] = -GSR_SH_C1 * SH(1, c); dz[c] = GSR_SH_C1 * SH(2, c);
         }
         if (deg > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            const float d4 = kSH_C2[0] * xy, d5 = kSH_C2[1] * yz, d6 = kSH_C2[2] * (2.f * zz - xx - yy);
-            const float d7 = kSH_C2[3] * xz, d8 = kSH_C2[4] * (xx - yy);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                DSH(4, c) = d4 * dRGB[c]; DSH(5, c) = d5 * dRGB[c]; DSH(6, c) = d6 * dRGB[c];
-                DSH(7, c) = d7 * dRGB[c]; DSH(8, c) = d8 * dRGB[c];
                 dx[c] += kSH_C2[0] * y * SH(4, c) + kSH_C2[2] * 2.f * -x * SH(6, c) + kSH_C2[3] * z * SH(7, c) +
                          kSH_C2[4] * 2.f * x * SH(8, c);
                 dy[c] += kSH_C2[0] * x * SH(4, c) + kSH_C2[1] * z * SH(5, c) + kSH_C2[2] * 2.f * -y * SH(6, c) +
@@ -210,18 +203,8 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *c
                 dz[c] += kSH_C2[1] * y * SH(5, c) + kSH_C2[2] * 2.f * 2.f * z * SH(6, c) + kSH_C2[3] * x * SH(7, c);
             }
             if (deg > 2) {
-                const float d9 = kSH_C3[0] * y * (3.f * xx - yy);
-                const float d10 = kSH_C3[1] * xy * z;
-                const float d11 = kSH_C3[2] * y * (4.f * zz - xx - yy);
-                const float d12 = kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                const float d13 = kSH_C3[4] * x * (4.f * zz - xx - yy);
-                const float d14 = kSH_C3[5] * z * (xx - yy);
-                const float d15 = kSH_C3[6] * x * (xx - 3.f * yy);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
-                    DSH(9, c) = d9 * dRGB[c]; DSH(10, c) = d10 * dRGB[c]; DSH(11, c) = d11 * dRGB[c];
-                    DSH(12, c) = d12 * dRGB[c]; DSH(13, c) = d13 * dRGB[c]; DSH(14, c) = d14 * dRGB[c];
-                    DSH(15, c) = d15 * dRGB[c];
                     dx[c] += (kSH_C3[0] * SH(9, c) * 3.f * 2.f * xy + kSH_C3[1] * SH(10, c) * yz +
                               kSH_C3[2] * SH(11, c) * -2.f * xy + kSH_C3[3] * SH(12, c) * -3.f * 2.f * xz +
                               kSH_C3[4] * SH(13, c) * (-3.f * xx + 4.f * zz - yy) +
@@ -238,7 +221,29 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *c
         }
     }
 #undef SH
-#undef DSH
+    // ---- phase 2: coefficient gradients (basis value x dL/dRGB) ----
+    float basis[16];
+    basis[0] = GSR_SH_C0;
+    basis[1] = -GSR_SH_C1 * y; basis[2] = GSR_SH_C1 * z; basis[3] = -GSR_SH_C1 * x;
+    basis[4] = kSH_C2[0] * xy; basis[5] = kSH_C2[1] * yz; basis[6] = kSH_C2[2] * (2.f * zz - xx - yy);
+    basis[7] = kSH_C2[3] * xz; basis[8] = kSH_C2[4] * (xx - yy);
+    basis[9] = kSH_C3[0] * y * (3.f * xx - yy);
+    basis[10] = kSH_C3[1] * xy * z;
+    basis[11] = kSH_C3[2] * y * (4.f * zz - xx - yy);
+    basis[12] = kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+    basis[13] = kSH_C3[4] * x * (4.f * zz - xx - yy);
+    basis[14] = kSH_C3[5] * z * (xx - yy);
+    basis[15] = kSH_C3[6] * x * (xx - 3.f * yy);
+    const int active = (deg + 1) * (deg + 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i < M) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = i < active ? basis[i] * dRGB[c] : 0.f;
+        }
+    }
+    for (int i = 16; i < M; ++i)
+        for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = 0.f;
     const float3 dL_ddir = make_float3(dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2],
                                        dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
                                        dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]);
@@ -281,18 +286,18 @@ __device__ inline void cov3d_backward(float3 s3, float mod, float4 q, const floa
 #undef G
 }
 
-__global__ __launch_bounds__(256) void k_gauss_bwd(
-    int P, int D, int M, int W, int H, float scale_modifier, float tan_fovx, float tan_fovy,
+template <int MC>
+__device__ inline void gauss_bwd_one(
+    int i, int D, int M, int W, int H, float scale_modifier, float tan_fovx, float tan_fovy,
     float h_x, float h_y, const float *__restrict__ means3D, const float *__restrict__ scales,
     const float *__restrict__ rotations, const float *__restrict__ shs,
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
     const float *__restrict__ projmatrix, const float *__restrict__ campos,
     const int *__restrict__ radii, const uint32_t *__restrict__ goff, const uint32_t *__restrict__ inv,
-    const float *__restrict__ partial, float *__restrict__ dL_dmeans2D, float *__restrict__ dL_dcolors,
-    float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D, float *__restrict__ dL_dcov3D,
-    float *__restrict__ dL_dsh, float *__restrict__ dL_dscales, float *__restrict__ dL_drot) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
+    const float4 *__restrict__ part8, const float *__restrict__ part1, float *__restrict__ dL_dmeans2D,
+    float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
+    float *__restrict__ dL_drot, float *s_row) {
     if (!(radii[i] > 0)) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -304,19 +309,34 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
         for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = 0.f;
 #pragma unroll
         for (int k = 0; k < 4; ++k) dL_drot[4 * i + k] = 0.f;
-        if (dL_dsh)
+        if (MC > 0) {
+#pragma unroll
+            for (int k = 0; k < 3 * MC; ++k) s_row[k] = 0.f;
+        } else if (dL_dsh) {
             for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
+        }
         return;
     }
-    // ---- sum the slot records of this Gaussian in emission order ----
+    // ---- sum the slot records of this Gaussian in emission order (4 slots in flight) ----
     float acc[kPartial];
 #pragma unroll
     for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
     const uint32_t e0 = goff[i], e1 = goff[i + 1];
-    for (uint32_t e = e0; e < e1; ++e) {
-        const float *src = partial + (size_t)inv[e] * kPartial;
+    for (uint32_t e = e0; e < e1; e += 4) {
+        uint32_t sl[4];
 #pragma unroll
-        for (int k = 0; k < kPartial; ++k) acc[k] += src[k];
+        for (int u = 0; u < 4; ++u) sl[u] = inv[min(e + u, e1 - 1)];
+        float4 pa[4], pb[4];
+        float pc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { pa[u] = part8[2 * (size_t)sl[u]]; pb[u] = part8[2 * (size_t)sl[u] + 1]; pc[u] = part1[sl[u]]; }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (e + u < e1) {
+                acc[0] += pa[u].x; acc[1] += pa[u].y; acc[2] += pa[u].z; acc[3] += pa[u].w;
+                acc[4] += pb[u].x; acc[5] += pb[u].y; acc[6] += pb[u].z; acc[7] += pb[u].w; acc[8] += pc[u];
+            }
+        }
     }
     dL_dmeans2D[3 * i] = acc[0]; dL_dmeans2D[3 * i + 1] = acc[1]; dL_dmeans2D[3 * i + 2] = 0.f;
     dL_dopacity[i] = acc[5];
@@ -415,10 +435,15 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     dm0 += (pj[0] * m_w - pj[3] * mul1) * g2x + (pj[1] * m_w - pj[3] * mul2) * g2y;
     dm1 += (pj[4] * m_w - pj[7] * mul1) * g2x + (pj[5] * m_w - pj[7] * mul2) * g2y;
     dm2 += (pj[8] * m_w - pj[11] * mul1) * g2x + (pj[9] * m_w - pj[11] * mul2) * g2y;
-    if (shs) {
+    if (MC > 0) {
+        bool cl[3];
+        (void)sh_to_rgb(D, mean, campos, s_row, cl);  // recompute the forward's clamp mask
+        const float3 d = sh_backward(D, MC, mean, campos, s_row, cl, make_float3(acc[6], acc[7], acc[8]), s_row);
+        dm0 += d.x; dm1 += d.y; dm2 += d.z;
+    } else if (shs) {
         const float *sh = shs + (size_t)i * M * 3;
         bool cl[3];
-        (void)sh_to_rgb(D, mean, campos, sh, cl);  // recompute the forward's clamp mask
+        (void)sh_to_rgb(D, mean, campos, sh, cl);
         const float3 d = sh_backward(D, M, mean, campos, sh, cl, make_float3(acc[6], acc[7], acc[8]),
                                      dL_dsh + (size_t)i * M * 3);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
@@ -437,6 +462,46 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     }
 }
 
+template <int MC>  // SH coefficient count staged through LDS (0: direct global access / no SH)
+__global__ __launch_bounds__(256) void k_gauss_bwd(
+    int P, int D, int M, int W, int H, float scale_modifier, float tan_fovx, float tan_fovy,
+    float h_x, float h_y, const float *__restrict__ means3D, const float *__restrict__ scales,
+    const float *__restrict__ rotations, const float *__restrict__ shs,
+    const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
+    const float *__restrict__ projmatrix, const float *__restrict__ campos,
+    const int *__restrict__ radii, const uint32_t *__restrict__ goff, const uint32_t *__restrict__ inv,
+    const float4 *__restrict__ part8, const float *__restrict__ part1, float *__restrict__ dL_dmeans2D,
+    float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
+    float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
+    float *__restrict__ dL_drot) {
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
+    const int i0 = blockIdx.x * kShBlock;
+    const int nrow = min(kShBlock, P - i0);
+    if (MC > 0) {  // coalesced copy of this block's SH rows into LDS (reused for dL/dSH)
+        const float *src = shs + (size_t)i0 * RL;
+        for (int e = threadIdx.x; e < nrow * RL; e += kShBlock) {
+            const int r = e / RL;
+            s_sh[r * RS + (e - r * RL)] = src[e];
+        }
+        __syncthreads();
+    }
+    const int i = i0 + threadIdx.x;
+    if (i < P) gauss_bwd_one<MC>(i, D, M, W, H, scale_modifier, tan_fovx, tan_fovy, h_x, h_y, means3D,
+                                 scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos,
+                                 radii, goff, inv, part8, part1, dL_dmeans2D, dL_dcolors, dL_dopacity,
+                                 dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS);
+    if (MC > 0) {  // coalesced store of the dL/dSH rows
+        __syncthreads();
+        float *dst = dL_dsh + (size_t)i0 * RL;
+        for (int e = threadIdx.x; e < nrow * RL; e += kShBlock) {
+            const int r = e / RL;
+            dst[e] = s_sh[r * RS + (e - r * RL)];
+        }
+    }
+}
+
+
 // ==========================================================================================
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
@@ -445,17 +510,28 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     k_render_bwd<<<div_up(T, kTilesPerBlock), 64 * kTilesPerBlock, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_b, a.ranges, a.point_list, a.rec, a.bg, a.final_T,
-                                  a.n_contrib, a.tile_maxc, a.dL_dcolor, a.partial);
+                                  a.n_contrib, a.tile_maxc, a.dL_dcolor, a.part8, a.part1);
     return hipGetLastError();
+}
+
+template <int MC>
+static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
+    k_gauss_bwd<MC><<<div_up(a.P, kShBlock), kShBlock, sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0), s>>>(
+        a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
+        a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
+        a.radii, a.goff, a.inv, a.part8, a.part1, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
+        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot);
 }
 
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {
     if (a.P == 0) return hipSuccess;
-    k_gauss_bwd<<<div_up(a.P, 256), 256, 0, s>>>(
-        a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
-        a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
-        a.radii, a.goff, a.inv, a.partial, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity, a.dL_dmeans3D,
-        a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot);
+    switch (a.shs ? a.M : 0) {
+        case 16: gauss_bwd_mc<16>(a, s); break;
+        case 9: gauss_bwd_mc<9>(a, s); break;
+        case 4: gauss_bwd_mc<4>(a, s); break;
+        case 1: gauss_bwd_mc<1>(a, s); break;
+        default: gauss_bwd_mc<0>(a, s); break;
+    }
     return hipGetLastError();
 }
 

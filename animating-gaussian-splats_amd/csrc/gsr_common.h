@@ -14,7 +14,7 @@ namespace gsr {
 constexpr int kTileW = 16;  // 16x16 pixel tiles (upstream BLOCK_X/BLOCK_Y)
 constexpr int kTileH = 16;
 constexpr int kTilePix = kTileW * kTileH;  // 256 = 4 wave64 per tile block
-constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic xyw, dopacity, dcolor rgb
+constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic abc, dopacity, dcolour rgb
 constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
 
 __host__ __device__ inline int div_up(int a, int b) { return (a + b - 1) / b; }
@@ -93,14 +93,23 @@ struct BinningLayout {
     }
 };
 
-// SCRATCH (backward): one 9-float partial-gradient record per sorted slot.
+// SCRATCH (backward): one 9-float partial-gradient record per sorted slot, split into a 32-byte
+// aligned part (dmean2D.xy, dconic.abc, dopacity, dcolour.rg) and the trailing dcolour.b.
 struct ScratchLayout {
-    size_t partial, total;
+    size_t part8, part1, total;
     __host__ __device__ ScratchLayout(int K) {
-        partial = 0;
-        total = align256(sizeof(float) * kPartial * size_t(K > 0 ? K : 1));
+        const size_t k = size_t(K > 0 ? K : 1);
+        size_t o = 0;
+        part8 = o; o = align256(o + sizeof(float4) * 2 * k);
+        part1 = o; o = align256(o + sizeof(float) * k);
+        total = o;
     }
 };
+
+// SH rows staged through LDS by the per-Gaussian kernels (coalesced global traffic): compile-time
+// coefficient counts for the degrees the reference can activate; other counts use direct loads.
+constexpr int kShBlock = 256;
+__host__ __device__ constexpr int sh_row_stride(int MC) { return (3 * MC) | 1; }  // odd: no bank conflicts
 
 // ---------------------------------------------------------------------------------------------
 // Device math -- same op order as oracle/gsr_oracle.c
@@ -194,9 +203,9 @@ __device__ inline float3 cov2d(float3 mean, float fx, float fy, float tfx, float
     return make_float3(GM(cov, 0, 0) + 0.3f, GM(cov, 0, 1), GM(cov, 1, 1) + 0.3f);
 }
 
-// SH -> RGB for one channel set; `sh` points at the Gaussian's (M,3) coefficients.
-__device__ inline float3 sh_to_rgb(int deg, float3 mean, const float *campos, const float *sh,
-                                   bool *clamped) {
+// SH -> RGB for one channel set; `sh` points at the Gaussian's (M,3) coefficients (global or LDS).
+template <typename ShPtr>
+__device__ inline float3 sh_to_rgb(int deg, float3 mean, const float *campos, ShPtr sh, bool *clamped) {
     float3 dir = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
     const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
     dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;

@@ -21,6 +21,7 @@
 namespace gsr {
 
 // ------------------------------------------------------------------------------------------
+template <int MC>  // SH coefficient count staged through LDS (0: direct loads / no SH)
 __global__ __launch_bounds__(256) void k_preprocess(
     int P, int D, int M, const float *__restrict__ means3D, const float *__restrict__ scales,
     float scale_modifier, const float *__restrict__ rotations, const float *__restrict__ opacities,
@@ -30,7 +31,19 @@ __global__ __launch_bounds__(256) void k_preprocess(
     float tan_fovx, float tan_fovy, float focal_x, float focal_y, int gx, int gy,
     int *__restrict__ radii, float *__restrict__ depth_out, float4 *__restrict__ rec_out,
     uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
+    const int i0 = blockIdx.x * kShBlock;
+    if (MC > 0) {  // coalesced copy of this block's SH rows into LDS
+        const int nrow = min(kShBlock, P - i0);
+        const float *src = shs + (size_t)i0 * RL;
+        for (int e = threadIdx.x; e < nrow * RL; e += kShBlock) {
+            const int r = e / RL;
+            s_sh[r * RS + (e - r * RL)] = src[e];
+        }
+        __syncthreads();
+    }
+    const int i = i0 + threadIdx.x;
     if (i >= P) return;
     // matrices are tiny and uniform: every lane reads the same words (scalar loads)
     float vm[16], pm[16];
@@ -72,7 +85,8 @@ __global__ __launch_bounds__(256) void k_preprocess(
         rgb = make_float3(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2]);
     } else {
         bool cl[3];
-        rgb = sh_to_rgb(D, p, campos, shs + (size_t)i * M * 3, cl);
+        if (MC > 0) rgb = sh_to_rgb(D, p, campos, s_sh + threadIdx.x * RS, cl);
+        else rgb = sh_to_rgb(D, p, campos, shs + (size_t)i * M * 3, cl);
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
@@ -409,12 +423,24 @@ __global__ void k_mark_visible(int P, const float *__restrict__ means3D,
 // ==========================================================================================
 // host launchers
 // ==========================================================================================
-hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {
-    if (a.P == 0) return hipSuccess;
-    k_preprocess<<<div_up(a.P, 256), 256, 0, s>>>(
+template <int MC>
+static void preprocess_mc(const FwdArgs &a, hipStream_t s) {
+    k_preprocess<MC><<<div_up(a.P, kShBlock), kShBlock, sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0), s>>>(
         a.P, a.D, a.M, a.means3D, a.scales, a.scale_modifier, a.rotations, a.opacities, a.shs,
         a.colors_precomp, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
         a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles);
+}
+
+hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {
+    if (a.P == 0) return hipSuccess;
+    const int mc = a.shs ? a.M : 0;
+    switch (mc) {
+        case 16: preprocess_mc<16>(a, s); break;
+        case 9: preprocess_mc<9>(a, s); break;
+        case 4: preprocess_mc<4>(a, s); break;
+        case 1: preprocess_mc<1>(a, s); break;
+        default: preprocess_mc<0>(a, s); break;
+    }
     return hipGetLastError();
 }
 

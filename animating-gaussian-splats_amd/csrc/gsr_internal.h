@@ -39,7 +39,7 @@ struct BwdArgs {
     const uint32_t *tile_maxc; const uint32_t *tile_cost; uint32_t *tile_order_b;
     const uint32_t *point_list; const uint32_t *inv;
     // scratch
-    float *partial;
+    float4 *part8; float *part1;
     // upstream gradient
     const float *dL_dcolor;
     // outputs

@@ -36,12 +36,16 @@ def _dump_stats():
 
 
 def _inputs(P, W, H, focal, s0, seed=0, sh_degree=-1, yaw=0.0, height=0.0, distance=4.0,
-            bg=(0.0, 0.0, 0.0)):
+            bg=(0.0, 0.0, 0.0), active_degree=None, extra_coeffs=0):
     p = S.synthetic_cloud(P, s0, sh_degree=sh_degree, seed=seed, device="cpu")
     a = {k: (v.detach() if isinstance(v, torch.Tensor) else v)
          for k, v in S.activated_inputs(p, sh_degree).items()}
+    if extra_coeffs:  # more stored coefficients than the active degree uses (generic M path)
+        g = torch.Generator().manual_seed(seed + 99)
+        a["shs"] = torch.cat([a["shs"], 0.05 * torch.randn(P, extra_coeffs, 3, generator=g)], 1).contiguous()
+    deg = max(sh_degree, 0) if active_degree is None else active_degree
     rs = S.render_settings(W, H, S.intrinsics(focal, W, H), S.look_at(yaw, height, distance),
-                           device="cpu", sh_degree=max(sh_degree, 0))
+                           device="cpu", sh_degree=deg)
     rs = rs._replace(bg=torch.tensor(bg, dtype=torch.float32))
     return a, rs
 
@@ -162,6 +166,10 @@ CASES = {
     "sh1_yaw": (5_000, 160, 96, 120.0, 0.03, 1, dict(yaw=90.0, height=0.8)),
     "sh3": (20_000, 480, 270, 400.0, 0.01, 3, {}),
     "dense_small": (4_000, 64, 48, 64.0, 0.08, -1, {}),
+    "sh0": (3_000, 96, 80, 80.0, 0.03, 0, {}),
+    "sh2": (3_000, 96, 80, 80.0, 0.03, 2, dict(yaw=200.0)),
+    "sh3_active2": (3_000, 96, 80, 80.0, 0.03, 3, dict(active_degree=2)),
+    "sh_m25_generic": (3_000, 96, 80, 80.0, 0.03, 3, dict(extra_coeffs=9)),
 }
 
 
