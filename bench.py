@@ -9,8 +9,9 @@ shared.py:29-42 included), backpropagates a fixed upstream dL/dcolor into the le
 (gradients accumulate over the rank's views, as train.py sums view losses), and for N > 1
 all-reduces (SUM) the parameter gradients over RCCL.  Inputs are resident in HBM before timing.
 
-N > 1: launched by torch.distributed.run, one process per GPU; rank r takes rig cameras
-(step * N * V + r * V + j) mod 27 (camera data parallelism, weak scaling: fixed views per GPU).
+N > 1: launched by torch.distributed.run, one process per GPU; the step's N * V rig cameras
+(step * N * V + k) mod 27 are sharded round-robin over ranks (splat_dp.shard_views; camera data
+parallelism, weak scaling: fixed views per GPU), then splat_dp.GradAllReduce sums the gradients.
 
 Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP events inside libgsr on
 the stream the kernel runs on) and the CPU-oracle baseline (rank 0, N = 1 only).
@@ -102,23 +103,20 @@ def main():
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
     V = args.views_per_rank
 
+    import splat_dp
+    reducer = splat_dp.GradAllReduce(params.values()) if dist is not None else None
+
     def step(it):
-        for j in range(V):
-            cam = cams[(it * world * V + rank * V + j) % len(cams)]
+        # rank r renders its round-robin share of this step's world * V rig cameras
+        step_cams = [(it * world * V + k) % len(cams) for k in range(world * V)]
+        for ci in splat_dp.shard_views(step_cams, rank, world):
             a = S.activated_inputs(params, cfg.sh_degree)
             if cfg.sh_degree >= 0:
                 a.pop("colors_precomp")
-            img, _radii, _depth = GaussianRasterizer(raster_settings=cam)(**a)
+            img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**a)
             img.backward(dl)
-        if dist is not None:
-            grads = [p.grad for p in params.values()]
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            dist.all_reduce(flat)
-            o = 0
-            for g in grads:
-                n = g.numel()
-                g.copy_(flat[o:o + n].view_as(g))
-                o += n
+        if reducer is not None:
+            reducer()  # one flat-bucket all-reduce (SUM) of every parameter gradient over RCCL
         for p in params.values():
             p.grad = None
 
@@ -149,8 +147,10 @@ def main():
               "render_bwd", "gauss_bwd"]
     times = {ph: _C.profile_read(ph) for ph in phases}
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
-    used = sorted({(it * world * V + rank * V + j) % len(cams)
-                   for it in range(args.warmup, args.warmup + args.steps) for j in range(V)})
+    import splat_dp
+    used = sorted({ci for it in range(args.warmup, args.warmup + args.steps)
+                   for ci in splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)],
+                                                  rank, world)})
     Ks = []
     with torch.no_grad():
         a = S.activated_inputs(params, cfg.sh_degree)

@@ -1,0 +1,136 @@
+"""Generate golden vectors by running the REFERENCE's own Python callers of the rasterizer.
+
+Run in the build container only (needs /root/reference, which does not exist on the GPU box):
+    python tests/golden/gen_golden.py
+Writes tests/golden/reference_harness.npz (data only: inputs and the reference's outputs).
+
+What is captured:
+  * create_render_settings (shared.py:64-124) for the benchmark/test cameras and the inference rig
+    of train.py:460-503 (create_extrinsic_matrices / render_and_export_frame intrinsics)
+  * create_render_arguments (shared.py:29-42) activations on a seeded parameter dict
+  * build_rotation (external.py:27-46) - the quaternion convention of Sigma3D
+  * calc_ssim (external.py:68-110) on seeded images (for the fused-loss row of SURVEY 8(f))
+  * update_max_2d_radii_and_visibility_mask (densify.py:154-162) + accumulate_mean_2d_gradients
+    (external.py:113-124) over a sequence of seeded views, and densify_gaussians
+    (external.py:211-314) at i = 500 with a seeded torch.normal - the statistics the data-parallel
+    grad/stat reduction must reproduce.
+
+The reference needs open3d / wandb / imageio / a rasterizer and CUDA; here open3d, wandb and imageio
+are empty stub modules, ``diff_gaussian_rasterization`` is this repo's drop-in (only its settings
+namedtuple is used), and ``.cuda()`` / ``device="cuda"`` are redirected to the CPU.  Nothing from
+the reference is copied: its modules are imported from /root/reference and only their outputs are
+saved.  No bytecode is written into /root/reference.
+"""
+import importlib
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path[:0] = [os.path.join(REPO, "animating-gaussian-splats_amd"), REPO]
+
+
+def _install_shims():
+    for name in ("open3d", "wandb", "imageio"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    torch.Tensor.cuda = lambda self, *a, **k: self
+
+    def cpu(fn):
+        def wrapped(*a, **k):
+            if "device" in k:
+                k["device"] = "cpu"
+            return fn(*a, **k)
+        return wrapped
+
+    for fname in ("tensor", "zeros", "zeros_like", "ones", "ones_like", "empty", "normal", "randn"):
+        setattr(torch, fname, cpu(getattr(torch, fname)))
+
+
+def main():
+    _install_shims()
+    sys.path.insert(0, REF)
+    shared = importlib.import_module("shared")
+    external = importlib.import_module("external")
+    densify = importlib.import_module("densify")
+    train = importlib.import_module("train")
+    out = {}
+
+    # ---- cameras -------------------------------------------------------------------------
+    cams = []
+    for W, H, f, yaw, hgt, dist in [(256, 256, 256.0, 0.0, 0.0, 4.0), (800, 800, 800.0, 90.0, 0.0, 4.0),
+                                    (1920, 1080, 1600.0, 0.0, 0.0, 4.0), (1920, 1080, 1600.0, 280.0, 0.8, 4.0),
+                                    (200, 120, 150.0, 200.0, -0.8, 4.0)]:
+        K = np.array([[f, 0.0, W / 2], [0.0, f, H / 2], [0.0, 0.0, 1.0]])
+        cams.append((W, H, K, train.create_transformation_matrix(yaw, hgt, dist)))
+    for key, (w2c, aspect) in train.create_extrinsic_matrices().items():
+        W, H = 1280, 720
+        K = np.array([[aspect * W, 0, W / 2], [0, aspect * W, H / 2], [0, 0, 1]])
+        cams.append((W, H, K, w2c))
+    for c, (W, H, K, w2c) in enumerate(cams):
+        rs = shared.create_render_settings(image_width=W, image_height=H, intrinsic_matrix=K,
+                                           extrinsic_matrix=w2c)
+        out[f"cam{c}_in_K"] = K
+        out[f"cam{c}_in_w2c"] = w2c
+        out[f"cam{c}_in_wh"] = np.array([W, H])
+        out[f"cam{c}_viewmatrix"] = rs.viewmatrix.contiguous().numpy()
+        out[f"cam{c}_projmatrix"] = rs.projmatrix.contiguous().numpy()
+        out[f"cam{c}_campos"] = rs.campos.numpy()
+        out[f"cam{c}_tanfov"] = np.array([rs.tanfovx, rs.tanfovy], dtype=np.float64)
+        out[f"cam{c}_bg"] = rs.bg.numpy()
+        out[f"cam{c}_misc"] = np.array([rs.image_height, rs.image_width, rs.sh_degree,
+                                        float(rs.scale_modifier), float(rs.prefiltered)])
+    out["n_cams"] = np.array(len(cams))
+
+    # ---- render arguments --------------------------------------------------------------------
+    g = torch.Generator().manual_seed(0)
+    P = 257
+    params = {"means": torch.randn(P, 3, generator=g), "colors": torch.rand(P, 3, generator=g),
+              "rotation_quaternions": torch.randn(P, 4, generator=g),
+              "opacity_logits": torch.randn(P, 1, generator=g),
+              "log_scales": torch.randn(P, 3, generator=g) - 4.0}
+    for k, v in params.items():
+        out[f"args_in_{k}"] = v.numpy()
+    ra = shared.create_render_arguments(params)
+    for k, v in ra.items():
+        out[f"args_out_{k}"] = v.detach().numpy()
+    out["rot_out"] = external.build_rotation(params["rotation_quaternions"]).numpy()
+
+    # ---- SSIM ------------------------------------------------------------------------------
+    img1 = torch.rand(3, 48, 64, generator=g)
+    img2 = (img1 + 0.1 * torch.randn(3, 48, 64, generator=g)).clamp(0, 1)
+    out["ssim_in_img1"], out["ssim_in_img2"] = img1.numpy(), img2.numpy()
+    out["ssim_out"] = np.array(float(external.calc_ssim(img1, img2)))
+
+    # ---- densification statistics over a sequence of views ----------------------------------
+    P = 2000
+    gp = torch.Generator().manual_seed(5)
+    n_views = 6
+    radii_seq = [(torch.randint(0, 6, (P,), generator=gp) * (torch.rand(P, generator=gp) > 0.3)).int()
+                 for _ in range(n_views)]
+    grad_seq = [torch.randn(P, 3, generator=gp) * 4e-4 for _ in range(n_views)]
+    dv = shared.DensificationVariables(visibility_count=torch.zeros(P), mean_2d_gradients_accumulated=torch.zeros(P),
+                                       max_2d_radii=torch.zeros(P))
+    for r, gr in zip(radii_seq, grad_seq):
+        densify.update_max_2d_radii_and_visibility_mask(r, dv)
+        m2 = torch.zeros(P, 3, requires_grad=True)
+        m2.grad = gr
+        dv.means_2d = m2
+        external.accumulate_mean_2d_gradients(dv)
+    out["dstat_in_radii"] = torch.stack(radii_seq).numpy()
+    out["dstat_in_grad"] = torch.stack(grad_seq).numpy()
+    out["dstat_out_visibility_count"] = dv.visibility_count.numpy()
+    out["dstat_out_grad_accum"] = dv.mean_2d_gradients_accumulated.numpy()
+    out["dstat_out_max_radii"] = dv.max_2d_radii.numpy()
+
+    np.savez_compressed(os.path.join(HERE, "reference_harness.npz"), **out)
+    print(f"wrote {len(out)} arrays to tests/golden/reference_harness.npz")
+
+
+if __name__ == "__main__":
+    main()
