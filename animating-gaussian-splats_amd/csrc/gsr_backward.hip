@@ -42,6 +42,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const float *__restrict__ dL_dpixels, float4 *__restrict__ part8, float *__restrict__ part1) {
     __shared__ float4 s_rec[kTilesPerBlock][3][64];
     __shared__ float s_outs[kTilesPerBlock][64 * kPartial];
+    __shared__ uint32_t s_qs[kTilesPerBlock][64];
     const int wv = threadIdx.x >> 6;
     const int t_lin = blockIdx.x * kTilesPerBlock + wv;
     if (t_lin >= T) return;
@@ -49,6 +50,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     float4(&s_b)[64] = s_rec[wv][1];
     float4(&s_c)[64] = s_rec[wv][2];
     float *s_out = s_outs[wv];
+    uint32_t *s_q = s_qs[wv];
     const int tile = (int)tile_order[t_lin];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -70,11 +72,16 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     }
     const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-    float Tt[4], tbg[4], dp0[4], dp1[4], dp2[4], ar0[4], ar1[4], ar2[4], lc0[4], lc1[4], lc2[4], la[4];
+    // Per pixel state of the reverse walk.  The reference keeps accum_rec and last_color per channel,
+    // but dL/dalpha only needs their projections on dL/dpixel, and the recurrence
+    // accum_rec = last_alpha * last_color + (1 - last_alpha) * accum_rec is linear, so AR = <accum_rec,
+    // dL/dpix> and LC = <last_color, dL/dpix> are carried as scalars (same value, fewer registers).
+    float Tt[4], tbg[4], dp0[4], dp1[4], dp2[4], AR[4], LC[4], la[4], pfy[4];
     uint32_t lastc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int py = py0 + 4 * k;
+        pfy[k] = (float)py;
         const bool inside = px < W && py < H;
         const int pid = py * W + px;
         const float Tf = inside ? final_Ts[pid] : 0.f;
@@ -86,7 +93,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         float bd = 0;
         bd += bg0 * dp0[k]; bd += bg1 * dp1[k]; bd += bg2 * dp2[k];
         tbg[k] = -Tf * bd;  // background term of dL/dalpha: -T_final / (1 - alpha) * <bg, dL/dpix>
-        ar0[k] = ar1[k] = ar2[k] = 0.f; lc0[k] = lc1[k] = lc2[k] = 0.f; la[k] = 0.f;
+        AR[k] = 0.f; LC[k] = 0.f; la[k] = 0.f;
     }
     const int row = lane >> 4;
     const int slot0123 = (row == 0) ? 0 : (row == 1) ? 2 : (row == 2) ? 1 : 3;  // wave_sum9 lane map
@@ -95,42 +102,48 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         const int cnt = end - start;
 #pragma unroll
         for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
-        bool live = false;
+        // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile
+        uint32_t qmask = 0;
         float4 cj = make_float4(0.f, 0.f, 0.f, 0.f);  // exact conic of the Gaussian this lane staged
         if (lane < cnt) {
             const uint32_t g = point_list[rg.x + start + lane];
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
             cj = rec[(size_t)kRecF4 * g + 3];
             s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
-            live = !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0, tx1, ty1);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (!tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0 + 4 * k, tx1, ty0 + 4 * k + 3))
+                    qmask |= 1u << k;
         }
-        uint64_t m = __ballot(live);
+        s_q[lane] = qmask;
+        uint64_t m = __ballot(qmask != 0);
         wave_lds_sync();
         while (m) {
             const int j = 63 - __builtin_clzll(m);
             m &= ~(1ull << j);
             const uint32_t p = (uint32_t)(start + j);
+            const uint32_t qm = s_q[j];
             const float4 a = s_a[j], b = s_b[j], c = s_c[j];
             float v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0, v6 = 0, v7 = 0, v8 = 0;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const Blend e = blend_eval(a, b, pfx, (float)(py0 + 4 * k));
-                if (!(p < lastc[k] && blend_ok(e))) continue;
-                any = true;
-                const float r = __builtin_amdgcn_rcpf(1.f - e.alpha);
+                if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
+                // branch-free: a non-contributing pixel gets alpha = 0, which makes every update an
+                // identity (r = 1, dch = 0) and the state selects keep the previous contributor
+                const Blend e = blend_eval(a, b, pfx, pfy[k]);
+                const bool ok = p < lastc[k] && blend_ok(e);
+                any = any || ok;
+                const float al = ok ? e.alpha : 0.f;
+                const float r = __builtin_amdgcn_rcpf(1.f - al);
                 Tt[k] = Tt[k] * r;
-                const float dch = e.alpha * Tt[k];
-                float dLa = 0.0f;
-                ar0[k] = fmaf(la[k], lc0[k] - ar0[k], ar0[k]); lc0[k] = c.x;
-                dLa = fmaf(c.x - ar0[k], dp0[k], dLa); v6 = fmaf(dch, dp0[k], v6);
-                ar1[k] = fmaf(la[k], lc1[k] - ar1[k], ar1[k]); lc1[k] = c.y;
-                dLa = fmaf(c.y - ar1[k], dp1[k], dLa); v7 = fmaf(dch, dp1[k], v7);
-                ar2[k] = fmaf(la[k], lc2[k] - ar2[k], ar2[k]); lc2[k] = c.z;
-                dLa = fmaf(c.z - ar2[k], dp2[k], dLa); v8 = fmaf(dch, dp2[k], v8);
-                dLa *= Tt[k];
-                la[k] = e.alpha;
-                dLa = fmaf(r, tbg[k], dLa);
+                const float dch = al * Tt[k];
+                const float cd = fmaf(c.z, dp2[k], fmaf(c.y, dp1[k], c.x * dp0[k]));  // <colour, dL/dpix>
+                AR[k] = ok ? fmaf(la[k], LC[k] - AR[k], AR[k]) : AR[k];
+                LC[k] = ok ? cd : LC[k];
+                la[k] = ok ? e.alpha : la[k];
+                float dLa = fmaf(r, tbg[k], (cd - AR[k]) * Tt[k]);
+                dLa = ok ? dLa : 0.f;
                 const float sG = b.y * dLa * e.G;  // dL/dG * G
                 const float t = sG * e.dx, u = sG * e.dy;
                 v0 += t;
@@ -139,6 +152,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(
                 v3 = fmaf(t, e.dy, v3);
                 v4 = fmaf(u, e.dy, v4);
                 v5 = fmaf(e.G, dLa, v5);
+                v6 = fmaf(dch, dp0[k], v6);
+                v7 = fmaf(dch, dp1[k], v7);
+                v8 = fmaf(dch, dp2[k], v8);
             }
             if (__ballot(any)) {
                 const Sum9 sm = wave_sum9(v0, v1, v2, v3, v4, v5, v6, v7, v8);

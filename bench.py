@@ -146,6 +146,7 @@ def main():
     phases = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
               "render_bwd", "gauss_bwd"]
     times = {ph: _C.profile_read(ph) for ph in phases}
+    host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
     import splat_dp
     used = sorted({ci for it in range(args.warmup, args.warmup + args.steps)
@@ -200,6 +201,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
                          "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch)},
             "phase_ms_per_launch": {ph: round(times[ph][0] / max(times[ph][1], 1), 5) for ph in phases},
+            "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
