@@ -158,8 +158,9 @@ void carve_image(FwdArgs &a, char *base) {
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K);
-    a.keys = (uint64_t *)(base + L.keys); a.point_list = (uint32_t *)(base + L.point_list);
-    a.inv = (uint32_t *)(base + L.inv);
+    a.keys = (uint64_t *)(base + L.keys); a.vals = (uint32_t *)(base + L.vals);
+    a.point_list = (uint32_t *)(base + L.point_list);
+    a.slot_emit = (uint32_t *)(base + L.slot_emit);
 }
 
 }  // namespace
@@ -180,7 +181,7 @@ int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const BinningLayout b(K);
     const size_t v[12] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
                           im.ranges, im.final_T, im.n_contrib, im.tile_maxc,
-                          b.keys, b.point_list, b.inv};
+                          b.keys, b.point_list, b.slot_emit};
     int n = 0;
     for (; n < 12 && n < max_out; ++n) out[n] = v[n];
     return n;
@@ -284,7 +285,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff;
     a.ranges = f.ranges; a.final_T = f.final_T; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
     a.tile_cost = f.tile_cost; a.tile_order_b = f.tile_order_b;
-    a.point_list = f.point_list; a.inv = f.inv;
+    a.point_list = f.point_list; a.slot_emit = f.slot_emit;
     a.dL_dcolor = dL_dcolor;
     a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
     a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = out->dL_dsh;
@@ -292,8 +293,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, ScratchLayout(num_rendered).total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
     const ScratchLayout SL(num_rendered);
-    a.part8 = (float4 *)(scr + SL.part8);
-    a.part1 = (float *)(scr + SL.part1);
+    a.part = (float4 *)(scr + SL.part);
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
     { Phase ph(s, "gauss_bwd"); HIP_TRY(launch_gauss_bwd(a, s)); }
     return GSR_OK;

@@ -39,7 +39,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const uint32_t *__restrict__ point_list,
     const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
-    const float *__restrict__ dL_dpixels, float4 *__restrict__ part8, float *__restrict__ part1) {
+    const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
+    float4 *__restrict__ part) {
     __shared__ float4 s_rec[kTilesPerBlock][3][64];
     __shared__ float s_outs[kTilesPerBlock][64 * kPartial];
     __shared__ uint32_t s_qs[kTilesPerBlock][64];
@@ -65,10 +66,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
     const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
     for (int p = maxc + lane; p < n; p += 64) {  // slots nobody reached: zero records
-        const size_t sl = rg.x + p;
-        part8[2 * sl] = make_float4(0.f, 0.f, 0.f, 0.f);
-        part8[2 * sl + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        part1[sl] = 0.f;
+        float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
+        dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dst[2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
@@ -105,8 +106,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile
         uint32_t qmask = 0;
         float4 cj = make_float4(0.f, 0.f, 0.f, 0.f);  // exact conic of the Gaussian this lane staged
+        uint32_t em = 0;                              // emission index of the pair this lane staged
         if (lane < cnt) {
             const uint32_t g = point_list[rg.x + start + lane];
+            em = slot_emit[rg.x + start + lane];
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
             cj = rec[(size_t)kRecF4 * g + 3];
             s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
@@ -169,13 +172,13 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         if (lane < cnt) {
             const float *sm = s_out + lane * kPartial;
             const float S1 = sm[0], S2 = sm[1];
-            const size_t sl = rg.x + start + lane;
-            part8[2 * sl] = make_float4((-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
-                                        (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
-                                        -0.5f * sm[2],                       // dL/dconic.a
-                                        -0.5f * sm[3]);                      // dL/dconic.b (b/2 convention)
-            part8[2 * sl + 1] = make_float4(-0.5f * sm[4], sm[5], sm[6], sm[7]);  // dconic.c, dopacity, dcolour.rg
-            part1[sl] = sm[8];                                                    // dcolour.b
+            float4 *dst = part + 3 * (size_t)em;
+            dst[0] = make_float4((-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
+                                 (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
+                                 -0.5f * sm[2],                       // dL/dconic.a
+                                 -0.5f * sm[3]);                      // dL/dconic.b (b/2 convention)
+            dst[1] = make_float4(-0.5f * sm[4], sm[5], sm[6], sm[7]);  // dconic.c, dopacity, dcolour.rg
+            dst[2] = make_float4(sm[8], 0.f, 0.f, 0.f);                // dcolour.b
         }
     }
 }
@@ -309,8 +312,8 @@ __device__ inline void gauss_bwd_one(
     const float *__restrict__ rotations, const float *__restrict__ shs,
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
     const float *__restrict__ projmatrix, const float *__restrict__ campos,
-    const int *__restrict__ radii, const uint32_t *__restrict__ goff, const uint32_t *__restrict__ inv,
-    const float4 *__restrict__ part8, const float *__restrict__ part1, float *__restrict__ dL_dmeans2D,
+    const int *__restrict__ radii, const uint32_t *__restrict__ goff,
+    const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drot, float *s_row) {
@@ -333,26 +336,15 @@ __device__ inline void gauss_bwd_one(
         }
         return;
     }
-    // ---- sum the slot records of this Gaussian in emission order (4 slots in flight) ----
+    // ---- sum this Gaussian's pair records (contiguous, emission order) ----
     float acc[kPartial];
 #pragma unroll
     for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
     const uint32_t e0 = goff[i], e1 = goff[i + 1];
-    for (uint32_t e = e0; e < e1; e += 4) {
-        uint32_t sl[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) sl[u] = inv[min(e + u, e1 - 1)];
-        float4 pa[4], pb[4];
-        float pc[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) { pa[u] = part8[2 * (size_t)sl[u]]; pb[u] = part8[2 * (size_t)sl[u] + 1]; pc[u] = part1[sl[u]]; }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (e + u < e1) {
-                acc[0] += pa[u].x; acc[1] += pa[u].y; acc[2] += pa[u].z; acc[3] += pa[u].w;
-                acc[4] += pb[u].x; acc[5] += pb[u].y; acc[6] += pb[u].z; acc[7] += pb[u].w; acc[8] += pc[u];
-            }
-        }
+    for (uint32_t e = e0; e < e1; ++e) {
+        const float4 pa = part[3 * (size_t)e], pb = part[3 * (size_t)e + 1], pc = part[3 * (size_t)e + 2];
+        acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
+        acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc.x;
     }
     dL_dmeans2D[3 * i] = acc[0]; dL_dmeans2D[3 * i + 1] = acc[1]; dL_dmeans2D[3 * i + 2] = 0.f;
     dL_dopacity[i] = acc[5];
@@ -485,8 +477,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     const float *__restrict__ rotations, const float *__restrict__ shs,
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
     const float *__restrict__ projmatrix, const float *__restrict__ campos,
-    const int *__restrict__ radii, const uint32_t *__restrict__ goff, const uint32_t *__restrict__ inv,
-    const float4 *__restrict__ part8, const float *__restrict__ part1, float *__restrict__ dL_dmeans2D,
+    const int *__restrict__ radii, const uint32_t *__restrict__ goff,
+    const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drot) {
@@ -505,7 +497,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     const int i = i0 + threadIdx.x;
     if (i < P) gauss_bwd_one<MC>(i, D, M, W, H, scale_modifier, tan_fovx, tan_fovy, h_x, h_y, means3D,
                                  scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos,
-                                 radii, goff, inv, part8, part1, dL_dmeans2D, dL_dcolors, dL_dopacity,
+                                 radii, goff, part, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS);
     if (MC > 0) {  // coalesced store of the dL/dSH rows
         __syncthreads();
@@ -526,7 +518,7 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     k_render_bwd<<<div_up(T, kTilesPerBlock), 64 * kTilesPerBlock, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_b, a.ranges, a.point_list, a.rec, a.bg, a.final_T,
-                                  a.n_contrib, a.tile_maxc, a.dL_dcolor, a.part8, a.part1);
+                                  a.n_contrib, a.tile_maxc, a.slot_emit, a.dL_dcolor, a.part);
     return hipGetLastError();
 }
 
@@ -535,7 +527,7 @@ static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
     k_gauss_bwd<MC><<<div_up(a.P, kShBlock), kShBlock, sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0), s>>>(
         a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
         a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
-        a.radii, a.goff, a.inv, a.part8, a.part1, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
+        a.radii, a.goff, a.part, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
         a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot);
 }
 

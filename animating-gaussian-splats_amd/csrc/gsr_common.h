@@ -81,28 +81,30 @@ struct ImageLayout {
     }
 };
 
-// BINNING (per Gaussian-tile pair, K): sort keys, sorted Gaussian list, emission -> slot map.
+// BINNING (per Gaussian-tile pair, K): sort keys + their emission index, sorted Gaussian list,
+// emission index of every sorted slot (where the backward stores the slot's gradient record).
 struct BinningLayout {
-    size_t keys, point_list, inv, total;
+    size_t keys, vals, point_list, slot_emit, total;
     __host__ __device__ BinningLayout(int K) {
         size_t o = 0;
         keys = o;       o = align256(o + sizeof(uint64_t) * (K > 0 ? K : 1));
+        vals = o;       o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));  // emission index of each key
         point_list = o; o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
-        inv = o;        o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
+        slot_emit = o;  o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));  // sorted slot -> emission
         total = o;
     }
 };
 
-// SCRATCH (backward): one 9-float partial-gradient record per sorted slot, split into a 32-byte
-// aligned part (dmean2D.xy, dconic.abc, dopacity, dcolour.rg) and the trailing dcolour.b.
+// SCRATCH (backward): one 48-byte partial-gradient record per Gaussian-tile pair, stored at the
+// pair's EMISSION index (Gaussian-major), so each Gaussian's records are contiguous for the
+// per-Gaussian reduction: (dmean2D.xy, dconic.a, dconic.b) (dconic.c, dopacity, dcolour.rg)
+// (dcolour.b, -, -, -).
 struct ScratchLayout {
-    size_t part8, part1, total;
+    size_t part, total;
     __host__ __device__ ScratchLayout(int K) {
         const size_t k = size_t(K > 0 ? K : 1);
-        size_t o = 0;
-        part8 = o; o = align256(o + sizeof(float4) * 2 * k);
-        part1 = o; o = align256(o + sizeof(float) * k);
-        total = o;
+        part = 0;
+        total = align256(sizeof(float4) * 3 * k);
     }
 };
 

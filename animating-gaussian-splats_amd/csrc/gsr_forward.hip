@@ -200,7 +200,8 @@ __global__ __launch_bounds__(256) void k_bin_emit(int P, int CH, int T, int gx,
                                                   const uint32_t *__restrict__ block_off,
                                                   uint32_t *__restrict__ tile_cursor,
                                                   uint32_t *__restrict__ goff,
-                                                  uint64_t *__restrict__ keys, uint32_t K) {
+                                                  uint64_t *__restrict__ keys,
+                                                  uint32_t *__restrict__ vals, uint32_t K) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
     __shared__ uint32_t s_red[16];
     const int b = blockIdx.x;
@@ -237,11 +238,13 @@ __global__ __launch_bounds__(256) void k_bin_emit(int P, int CH, int T, int gx,
                 const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
                 const uint64_t key_lo = (uint64_t)(uint32_t)g;
                 const uint64_t key = ((uint64_t)__float_as_uint(depth[g]) << 32) | key_lo;
+                uint32_t e = ex;  // emission index: y-major over the rect, as the reference emits
                 for (int y = y0; y < y1; ++y)
-                    for (int x = x0; x < x1; ++x) {
+                    for (int x = x0; x < x1; ++x, ++e) {
                         const int t = y * gx + x;
                         const uint32_t pos = USE_LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_cursor[t], 1u);
                         keys[pos] = key;
+                        vals[pos] = e;
                     }
             }
         }
@@ -254,12 +257,124 @@ __global__ __launch_bounds__(256) void k_bin_emit(int P, int CH, int T, int gx,
 __device__ inline void tile_sort_write(uint64_t key, uint32_t slot, int tx, int ty,
                                        const uint2 *__restrict__ rects,
                                        const uint32_t *__restrict__ goff,
-                                       uint32_t *__restrict__ point_list, uint32_t *__restrict__ inv) {
+                                       uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit) {
     const uint32_t g = (uint32_t)key;
     point_list[slot] = g;
     const uint2 r = rects[g];
     const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF;
-    inv[goff[g] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0))] = slot;  // y-major emission order
+    slot_emit[slot] = goff[g] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));  // y-major emission order
+}
+
+// ---- wave-level register bitonic sort (gfx950 cross-lane ops) ------------------------------
+// Element i = lane * R + r lives in register r of `lane`: exchanges at distance < R stay inside a
+// lane, larger distances are lane xors d = dist / R done with DPP (d = 1, 2), ds_swizzle
+// (d = 4, 8, 16) or v_permlane32_swap (d = 32).
+template <int D>
+__device__ inline uint32_t lane_xor(uint32_t x) {
+    if constexpr (D == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+    else if constexpr (D == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+    else if constexpr (D == 4 || D == 8 || D == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (D << 10));
+    else {
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+}
+
+template <int R, int D>
+__device__ inline void bitonic_xlane(uint64_t (&k)[R], uint32_t (&v)[R], bool take_min) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t plo = lane_xor<D>((uint32_t)k[r]), phi = lane_xor<D>((uint32_t)(k[r] >> 32));
+        const uint32_t pv = lane_xor<D>(v[r]);
+        const uint64_t pk = ((uint64_t)phi << 32) | plo;
+        const bool mine = (k[r] < pk) == take_min;
+        k[r] = mine ? k[r] : pk;
+        v[r] = mine ? v[r] : pv;
+    }
+}
+
+template <int R>
+__device__ inline void wave_bitonic_kv(uint64_t (&k)[R], uint32_t (&v)[R], int lane) {
+#pragma clang loop unroll(full)
+    for (int kk = 2; kk <= 64 * R; kk <<= 1) {
+#pragma clang loop unroll(full)
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            if (j < R) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (r & j) continue;
+                    const int r2 = r | j;
+                    const bool asc = ((lane * R + r) & kk) == 0;
+                    if ((k[r] > k[r2]) == asc) {
+                        const uint64_t t = k[r]; k[r] = k[r2]; k[r2] = t;
+                        const uint32_t u = v[r]; v[r] = v[r2]; v[r2] = u;
+                    }
+                }
+            } else {
+                const int d = j / R;
+                const bool asc = ((lane * R) & kk) == 0;
+                const bool lower = (lane & d) == 0;
+                const bool take_min = lower == asc;
+                switch (d) {
+                    case 1: bitonic_xlane<R, 1>(k, v, take_min); break;
+                    case 2: bitonic_xlane<R, 2>(k, v, take_min); break;
+                    case 4: bitonic_xlane<R, 4>(k, v, take_min); break;
+                    case 8: bitonic_xlane<R, 8>(k, v, take_min); break;
+                    case 16: bitonic_xlane<R, 16>(k, v, take_min); break;
+                    default: bitonic_xlane<R, 32>(k, v, take_min); break;
+                }
+            }
+        }
+    }
+}
+
+template <int R>
+__device__ inline void tile_sort_regs(int n, uint32_t start, const uint64_t *__restrict__ keys,
+                                      const uint32_t *__restrict__ vals, uint32_t *__restrict__ point_list,
+                                      uint32_t *__restrict__ slot_emit, int lane) {
+    uint64_t k[R];
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane * R + r;
+        k[r] = i < n ? keys[start + i] : ~0ull;  // +inf padding sorts to the end
+        v[r] = i < n ? vals[start + i] : 0u;
+    }
+    wave_bitonic_kv<R>(k, v, lane);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int i = lane * R + r;
+        if (i < n) {
+            point_list[start + i] = (uint32_t)k[r];
+            slot_emit[start + i] = v[r];
+        }
+    }
+}
+
+// One wave per tile (4 tiles per block, no barriers), lists sorted entirely in registers.
+// LONG = false: tiles of 1..512 pairs (R <= 8); LONG = true: 513..1024 pairs (R = 16, more VGPRs,
+// separate launch so the short-list kernel keeps its occupancy).  Longer lists: k_tile_sort.
+constexpr int kRegSortMax = 1024;
+template <bool LONG>
+__global__ __launch_bounds__(256) void k_tile_sort_wave(int T, const uint2 *__restrict__ ranges,
+                                                        const uint64_t *__restrict__ keys,
+                                                        const uint32_t *__restrict__ vals,
+                                                        uint32_t *__restrict__ point_list,
+                                                        uint32_t *__restrict__ slot_emit) {
+    const int t = blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
+    if (t >= T) return;
+    const int lane = threadIdx.x & 63;
+    const uint2 rg = ranges[t];
+    const int n = (int)(rg.y - rg.x);
+    if (LONG) {
+        if (n > 512 && n <= kRegSortMax) tile_sort_regs<16>(n, rg.x, keys, vals, point_list, slot_emit, lane);
+        return;
+    }
+    if (n <= 0 || n > 512) return;
+    if (n <= 64) tile_sort_regs<1>(n, rg.x, keys, vals, point_list, slot_emit, lane);
+    else if (n <= 128) tile_sort_regs<2>(n, rg.x, keys, vals, point_list, slot_emit, lane);
+    else if (n <= 256) tile_sort_regs<4>(n, rg.x, keys, vals, point_list, slot_emit, lane);
+    else tile_sort_regs<8>(n, rg.x, keys, vals, point_list, slot_emit, lane);
 }
 
 __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restrict__ ranges,
@@ -267,12 +382,12 @@ __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restri
                                                    const uint2 *__restrict__ rects,
                                                    const uint32_t *__restrict__ goff,
                                                    uint32_t *__restrict__ point_list,
-                                                   uint32_t *__restrict__ inv) {
+                                                   uint32_t *__restrict__ slot_emit) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
     const int tile = blockIdx.x;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= 0) return;
+    if (n <= kRegSortMax) return;  // sorted in registers by k_tile_sort_wave
     const int tx = tile % gx, ty = tile / gx;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (n <= kSortCap) {
@@ -290,7 +405,7 @@ __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restri
                 }
                 __syncthreads();
             }
-        for (int i = tid; i < n; i += nt) tile_sort_write(s_keys[i], rg.x + i, tx, ty, rects, goff, point_list, inv);
+        for (int i = tid; i < n; i += nt) tile_sort_write(s_keys[i], rg.x + i, tx, ty, rects, goff, point_list, slot_emit);
     } else {
         // long tile: in-place bitonic network in global memory with virtual +inf padding
         // ("flip" form: every comparator puts the minimum at the lower index).
@@ -318,7 +433,7 @@ __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restri
                 __syncthreads();
             }
         }
-        for (int i = tid; i < n; i += nt) tile_sort_write(a[i], rg.x + i, tx, ty, rects, goff, point_list, inv);
+        for (int i = tid; i < n; i += nt) tile_sort_write(a[i], rg.x + i, tx, ty, rects, goff, point_list, slot_emit);
     }
 }
 
@@ -469,16 +584,22 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_emit<true><<<bg.NB, 256, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, (uint32_t)K);
+        k_bin_emit<true><<<bg.NB, 256, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
     else
-        k_bin_emit<false><<<bg.NB, 256, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, (uint32_t)K);
+        k_bin_emit<false><<<bg.NB, 256, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
+    k_tile_sort_wave<false><<<div_up(T, kTilesPerBlock), 256, 0, s>>>(T, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_tile_sort_wave<true><<<div_up(T, kTilesPerBlock), 256, 0, s>>>(T, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
     k_tile_sort<<<T, 256, sizeof(uint64_t) * kSortCap, s>>>(a.gx, a.ranges, a.keys, a.rect, a.goff,
-                                                            a.point_list, a.inv);
+                                                            a.point_list, a.slot_emit);
     return hipGetLastError();
 }
 

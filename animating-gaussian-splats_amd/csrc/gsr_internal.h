@@ -22,7 +22,7 @@ struct FwdArgs {
     uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
     // binning
-    uint64_t *keys; uint32_t *point_list; uint32_t *inv;
+    uint64_t *keys; uint32_t *vals; uint32_t *point_list; uint32_t *slot_emit;
     // outputs
     int *radii; float *out_color; float *out_depth;
 };
@@ -37,9 +37,9 @@ struct BwdArgs {
     const float4 *rec; const uint2 *rect;
     const uint32_t *goff; const uint2 *ranges; const float *final_T; const uint32_t *n_contrib;
     const uint32_t *tile_maxc; const uint32_t *tile_cost; uint32_t *tile_order_b;
-    const uint32_t *point_list; const uint32_t *inv;
+    const uint32_t *point_list; const uint32_t *slot_emit;
     // scratch
-    float4 *part8; float *part1;
+    float4 *part;
     // upstream gradient
     const float *dL_dcolor;
     // outputs

@@ -272,5 +272,5 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
         "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
         "keys": view(binningBuffer, o[9], K, i64, (K,)),
         "point_list": view(binningBuffer, o[10], K, i32, (K,)),
-        "inv": view(binningBuffer, o[11], K, i32, (K,)),
+        "slot_emit": view(binningBuffer, o[11], K, i32, (K,)),
     }
