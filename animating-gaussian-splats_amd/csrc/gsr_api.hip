@@ -46,6 +46,7 @@ int fail(int code, const char *fmt, ...) {
 struct ProfRec { std::string phase; hipEvent_t a, b; };
 std::mutex g_prof_mu;
 bool g_prof_on = false;
+std::string g_prof_sel;  // ",a,b," filter; empty = every phase
 std::vector<ProfRec> g_prof;
 std::vector<hipEvent_t> g_evpool;
 std::map<std::string, double> g_host_ms;
@@ -63,6 +64,7 @@ struct Phase {
     Phase(hipStream_t s_, const char *n) : s(s_), name(n) {
         if (!g_prof_on) return;
         std::lock_guard<std::mutex> lk(g_prof_mu);
+        if (!g_prof_sel.empty() && g_prof_sel.find("," + std::string(n) + ",") == std::string::npos) return;
         a = ev_get(); b = ev_get();
         if (a) (void)hipEventRecord(a, s);
     }
@@ -81,7 +83,7 @@ HostWord pinned_word() {
     thread_local HostWord w;
     if (!w.h) {
         uint32_t *h = nullptr;
-        if (hipHostMalloc((void **)&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return w;
+        if (hipHostMalloc((void **)&h, 4 * kHostWords, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return w;
         uint32_t *d = nullptr;
         if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) { (void)hipHostFree(h); return w; }
         w.h = h; w.d = d;
@@ -152,6 +154,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.n_contrib = (uint32_t *)(base + L.n_contrib); a.tile_maxc = (uint32_t *)(base + L.tile_maxc);
     a.tile_cost = (uint32_t *)(base + L.tile_cost); a.tile_order_f = (uint32_t *)(base + L.tile_order_f);
     a.tile_order_b = (uint32_t *)(base + L.tile_order_b);
+    a.sort_lists = (uint32_t *)(base + L.sort_lists);
     a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
     a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
     a.meta = (uint32_t *)(base + L.meta);
@@ -246,7 +249,9 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
     carve_binning(a, bin, (int)K);
     { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, (int)K, s)); }
-    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, s)); }
+    uint32_t n_per_path[3];
+    for (int c = 0; c < 3; ++c) n_per_path[c] = __atomic_load_n(hw.h + 1 + c, __ATOMIC_ACQUIRE);
+    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_per_path, s)); }
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     return GSR_OK;
 }
@@ -311,6 +316,12 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 int gsr_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;
+    return GSR_OK;
+}
+
+int gsr_profile_select(const char *phases) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_sel = (phases && *phases) ? "," + std::string(phases) + "," : std::string();
     return GSR_OK;
 }
 

@@ -16,6 +16,11 @@ constexpr int kTileH = 16;
 constexpr int kTilePix = kTileW * kTileH;  // 256 = 4 wave64 per tile block
 constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic abc, dopacity, dcolour rgb
 constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
+constexpr int kRegSortShort = 512;   // lists up to this length: register sort, R <= 8 keys per lane
+constexpr int kRegSortMax = 1024;    // lists up to this length: register sort, R = 16
+// host-mapped words published by k_bin_scan: [0] = K (written last, release), [1..3] = number of
+// tiles on each sort path (short register / long register / LDS-global)
+constexpr int kHostWords = 4;
 
 __host__ __device__ inline int div_up(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -58,8 +63,8 @@ struct BinGrid {
 
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
 struct ImageLayout {
-    size_t ranges, final_T, n_contrib, tile_maxc, tile_cost, tile_order_f, tile_order_b, tile_count,
-        tile_cursor, block_sums, block_off, meta, total;
+    size_t ranges, final_T, n_contrib, tile_maxc, tile_cost, tile_order_f, tile_order_b, sort_lists,
+        tile_count, tile_cursor, block_sums, block_off, meta, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -72,6 +77,7 @@ struct ImageLayout {
         tile_cost = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter: sum of n_contrib
         tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
         tile_order_b = o; o = align256(o + sizeof(uint32_t) * T);    // backward dispatch order (LPT)
+        sort_lists = o;  o = align256(o + sizeof(uint32_t) * 3 * T);  // tiles per sort path (3 lists of T)
         tile_count = o;  o = align256(o + sizeof(uint32_t) * T);
         tile_cursor = o; o = align256(o + sizeof(uint32_t) * T);
         block_sums = o;  o = align256(o + sizeof(uint32_t) * (NB + 1));

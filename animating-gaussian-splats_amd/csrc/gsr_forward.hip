@@ -153,10 +153,13 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
                                                    const uint32_t *__restrict__ block_sums,
                                                    uint32_t *__restrict__ block_off,
                                                    uint32_t *__restrict__ meta,
-                                                   uint32_t *host_K,
-                                                   uint32_t *__restrict__ tile_order) {
+                                                   uint32_t *host_words,
+                                                   uint32_t *__restrict__ tile_order,
+                                                   uint32_t *__restrict__ sort_lists) {
     __shared__ uint32_t s_red[16];
     __shared__ uint32_t s_hist[kOrderBuckets];
+    __shared__ uint32_t s_cls[3];
+    if (threadIdx.x < 3) s_cls[threadIdx.x] = 0;
     uint32_t carry = 0;
     for (int base = 0; base < T; base += blockDim.x) {
         const int t = base + threadIdx.x;
@@ -178,11 +181,24 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
         if (b < NB) block_off[b] = ex;
         carry2 += tot;
     }
+    // tiles per sort path (exact classes, so the host launches exactly the blocks each path needs)
+    __syncthreads();
+    for (int t = threadIdx.x; t < T; t += blockDim.x) {
+        const uint32_t n = tile_count[t];
+        if (n == 0) continue;
+        const int c = n <= (uint32_t)kRegSortShort ? 0 : (n <= (uint32_t)kRegSortMax ? 1 : 2);
+        sort_lists[c * T + atomicAdd(&s_cls[c], 1u)] = (uint32_t)t;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
         meta[0] = carry;
-        // publish K straight into host-mapped pinned memory: the host spins on this word instead of
-        // paying a copy kernel + stream synchronisation (system-scope store, seen by the CPU)
-        if (host_K) __hip_atomic_store(host_K, carry, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        // publish straight into host-mapped pinned memory (the host spins on word 0): no copy
+        // kernel, no stream synchronisation.  K goes last with system-scope release.
+        if (host_words) {
+            for (int c = 0; c < 3; ++c)
+                __hip_atomic_store(host_words + 1 + c, s_cls[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_words, carry, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     // forward render dispatch order: longest tile lists first
     lpt_order(T, [&](int t) { return tile_count[t]; }, tile_order, s_hist, s_red);
@@ -354,40 +370,40 @@ __device__ inline void tile_sort_regs(int n, uint32_t start, const uint64_t *__r
 // One wave per tile (4 tiles per block, no barriers), lists sorted entirely in registers.
 // LONG = false: tiles of 1..512 pairs (R <= 8); LONG = true: 513..1024 pairs (R = 16, more VGPRs,
 // separate launch so the short-list kernel keeps its occupancy).  Longer lists: k_tile_sort.
-constexpr int kRegSortMax = 1024;
+// `tiles` holds exactly the tiles of this path (built by k_bin_scan).
 template <bool LONG>
-__global__ __launch_bounds__(256) void k_tile_sort_wave(int T, const uint2 *__restrict__ ranges,
+__global__ __launch_bounds__(256) void k_tile_sort_wave(int count, const uint32_t *__restrict__ tiles,
+                                                        const uint2 *__restrict__ ranges,
                                                         const uint64_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ vals,
                                                         uint32_t *__restrict__ point_list,
                                                         uint32_t *__restrict__ slot_emit) {
-    const int t = blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
-    if (t >= T) return;
+    const int w = blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
+    if (w >= count) return;
     const int lane = threadIdx.x & 63;
-    const uint2 rg = ranges[t];
+    const uint2 rg = ranges[tiles[w]];
     const int n = (int)(rg.y - rg.x);
     if (LONG) {
-        if (n > 512 && n <= kRegSortMax) tile_sort_regs<16>(n, rg.x, keys, vals, point_list, slot_emit, lane);
+        tile_sort_regs<16>(n, rg.x, keys, vals, point_list, slot_emit, lane);
         return;
     }
-    if (n <= 0 || n > 512) return;
     if (n <= 64) tile_sort_regs<1>(n, rg.x, keys, vals, point_list, slot_emit, lane);
     else if (n <= 128) tile_sort_regs<2>(n, rg.x, keys, vals, point_list, slot_emit, lane);
     else if (n <= 256) tile_sort_regs<4>(n, rg.x, keys, vals, point_list, slot_emit, lane);
     else tile_sort_regs<8>(n, rg.x, keys, vals, point_list, slot_emit, lane);
 }
 
-__global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint2 *__restrict__ ranges,
+__global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
+                                                   const uint2 *__restrict__ ranges,
                                                    uint64_t *__restrict__ keys,
                                                    const uint2 *__restrict__ rects,
                                                    const uint32_t *__restrict__ goff,
                                                    uint32_t *__restrict__ point_list,
                                                    uint32_t *__restrict__ slot_emit) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
-    const int tile = blockIdx.x;
+    const int tile = (int)tiles[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= kRegSortMax) return;  // sorted in registers by k_tile_sort_wave
     const int tx = tile % gx, ty = tile / gx;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (n <= kSortCap) {
@@ -572,10 +588,11 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_K, hipStream_t s) {
+hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s) {
     const BinGrid bg(a.P);
     k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
-                                  a.block_sums, a.block_off, a.meta, host_K, a.tile_order_f);
+                                  a.block_sums, a.block_off, a.meta, host_words, a.tile_order_f,
+                                  a.sort_lists);
     return hipGetLastError();
 }
 
@@ -590,16 +607,18 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s) {
+hipError_t launch_tile_sort(const FwdArgs &a, const uint32_t *n_per_path, hipStream_t s) {
     const int T = a.gx * a.gy;
-    k_tile_sort_wave<false><<<div_up(T, kTilesPerBlock), 256, 0, s>>>(T, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    k_tile_sort_wave<true><<<div_up(T, kTilesPerBlock), 256, 0, s>>>(T, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    k_tile_sort<<<T, 256, sizeof(uint64_t) * kSortCap, s>>>(a.gx, a.ranges, a.keys, a.rect, a.goff,
-                                                            a.point_list, a.slot_emit);
+    const uint32_t *lists = a.sort_lists;
+    if (n_per_path[0])
+        k_tile_sort_wave<false><<<div_up((int)n_per_path[0], kTilesPerBlock), 256, 0, s>>>(
+            (int)n_per_path[0], lists, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
+    if (n_per_path[1])
+        k_tile_sort_wave<true><<<div_up((int)n_per_path[1], kTilesPerBlock), 256, 0, s>>>(
+            (int)n_per_path[1], lists + T, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
+    if (n_per_path[2])
+        k_tile_sort<<<n_per_path[2], 256, sizeof(uint64_t) * kSortCap, s>>>(
+            a.gx, lists + 2 * T, a.ranges, a.keys, a.rect, a.goff, a.point_list, a.slot_emit);
     return hipGetLastError();
 }
 

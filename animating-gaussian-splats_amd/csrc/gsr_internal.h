@@ -19,7 +19,7 @@ struct FwdArgs {
     float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff;
     // image
     uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc; uint32_t *tile_cost;
-    uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *tile_count;
+    uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
     // binning
     uint64_t *keys; uint32_t *vals; uint32_t *point_list; uint32_t *slot_emit;
@@ -49,9 +49,9 @@ struct BwdArgs {
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);
 hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s);
-hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_K, hipStream_t s);
+hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s);
 hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s);
-hipError_t launch_tile_sort(const FwdArgs &a, hipStream_t s);
+hipError_t launch_tile_sort(const FwdArgs &a, const uint32_t *n_per_path, hipStream_t s);
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s);
 hipError_t launch_zero(float *p, size_t n, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,

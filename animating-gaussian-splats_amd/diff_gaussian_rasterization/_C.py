@@ -28,7 +28,7 @@ GSR_BUF_GEOM, GSR_BUF_BINNING, GSR_BUF_IMAGE, GSR_BUF_SCRATCH = 0, 1, 2, 3
 EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_bytes", "gsr_image_bytes",
     "gsr_binning_bytes", "gsr_scratch_bytes", "gsr_last_error", "gsr_abi_version",
-    "gsr_profile_enable", "gsr_profile_reset", "gsr_profile_read", "gsr_buffer_offsets",
+    "gsr_profile_enable", "gsr_profile_select", "gsr_profile_reset", "gsr_profile_read", "gsr_buffer_offsets",
 )
 
 
@@ -88,6 +88,8 @@ def load_library():
     L.gsr_profile_enable.argtypes = [i]
     L.gsr_profile_enable.restype = i
     L.gsr_profile_reset.restype = i
+    L.gsr_profile_select.argtypes = [ctypes.c_char_p]
+    L.gsr_profile_select.restype = i
     L.gsr_profile_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i)]
     L.gsr_profile_read.restype = i
     L.gsr_buffer_offsets.restype = i
@@ -227,6 +229,11 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 # ---- instrumentation (per-phase HIP-event timing inside libgsr) ----
 def profile_enable(on=True):
     _check(load_library().gsr_profile_enable(int(bool(on))))
+
+
+def profile_select(phases=None):
+    """Record device events only for ``phases`` (iterable of names; None = all phases)."""
+    _check(load_library().gsr_profile_select(",".join(phases).encode() if phases else None))
 
 
 def profile_reset():

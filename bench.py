@@ -29,6 +29,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+# rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh), corrected
+# per MI355X_MICROARCH.md (2 x FETCH_SIZE + WRITE_SIZE): HBM bytes per launch of each kernel
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_hbm_pmc.json")
+PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "render_bwd",
+          "gauss_bwd"]
 
 
 def algorithmic_bytes(phase, P, K, N, T, F, sh):
@@ -37,14 +42,14 @@ def algorithmic_bytes(phase, P, K, N, T, F, sh):
         return P * (44 + F) + P * 60
     if phase == "render_fwd":      # per pair: id + xy + conic/op + rgb/depth gather; per pixel outputs
         return K * 44 + N * 24 + T * 12
-    if phase == "render_bwd":      # per pair: id + gathers + 36 B partial record; per pixel state
-        return K * (44 + 36) + N * 20 + T * 12
-    if phase == "gauss_bwd":       # per Gaussian inputs + all gradient outputs; per pair slot + record
-        return P * (44 + F + 12) + P * (56 + F) + K * 40
-    if phase == "tile_sort":       # keys in, point list + inverse map out, per-Gaussian rect/goff
-        return K * (8 + 4 + 4 + 12)
-    if phase == "bin_emit":
-        return P * 16 + K * 8
+    if phase == "render_bwd":      # per pair: id + emission slot + 36 B gather + 36 B partial record
+        return K * (4 + 4 + 36 + 36) + N * 20 + T * 12
+    if phase == "gauss_bwd":       # per Gaussian inputs + all gradient outputs; per pair 36 B record
+        return P * (44 + F + 12) + P * (56 + F) + K * 36
+    if phase == "tile_sort":       # (depth|id) key + emission index in, point list + slot map out
+        return K * (8 + 4 + 4 + 4)
+    if phase == "bin_emit":        # rect + tile count + depth + offset per Gaussian; key + index out
+        return P * (16 + 4 + 4) + K * 12
     if phase == "bin_count":
         return P * 12 + T * 4
     return 0
@@ -77,6 +82,8 @@ def main():
     ap.add_argument("--views-per-rank", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe-steps", type=int, default=3,
+                    help="untimed steps with events on every phase (per-kernel breakdown)")
     args = ap.parse_args()
 
     import splat_scenes as S
@@ -122,15 +129,27 @@ def main():
 
     for it in range(args.warmup):
         step(it)
+    # untimed probe: events around every kernel (they add launch gaps, so not in the timed region)
     torch.cuda.synchronize()
+    _C.profile_reset()
+    _C.profile_select(None)
+    _C.profile_enable(True)
+    for it in range(args.probe_steps):
+        step(args.warmup + it)
+    torch.cuda.synchronize()
+    _C.profile_enable(False)
+    probe = {ph: _C.profile_read(ph) for ph in PHASES}
+    dom = max(PHASES, key=lambda ph: probe[ph][0])
+    # timed region: HIP events only around the dominant kernel (its roofline), host timers on
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     _C.profile_reset()
+    _C.profile_select([dom])
     _C.profile_enable(True)
     t0 = time.perf_counter()
     for it in range(args.steps):
-        step(args.warmup + it)
+        step(args.warmup + args.probe_steps + it)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -142,14 +161,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel device time inside the timed region (HIP events on the launch stream)
-    phases = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
-              "render_bwd", "gauss_bwd"]
-    times = {ph: _C.profile_read(ph) for ph in phases}
+    # dominant kernel's device time inside the timed region (HIP events on its launch stream)
+    tot_ms, cnt = _C.profile_read(dom)
+    _C.profile_select(None)
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
     import splat_dp
-    used = sorted({ci for it in range(args.warmup, args.warmup + args.steps)
+    used = sorted({ci for it in range(args.warmup + args.probe_steps, args.warmup + args.probe_steps + args.steps)
                    for ci in splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)],
                                                   rank, world)})
     Ks = []
@@ -170,9 +188,12 @@ def main():
     N = cfg.width * cfg.height
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
     F = 12 * (cfg.sh_degree + 1) ** 2 if cfg.sh_degree >= 0 else 12
-    dom = max(phases, key=lambda ph: times[ph][0])
-    tot_ms, cnt = times[dom]
     avg_ms = tot_ms / max(cnt, 1)
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        pm = json.load(open(PMC_SUMMARY)).get("k_" + dom)
+        if pm:
+            traffic = int(pm["hbm_bytes_per_launch_corrected"])
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, cfg.sh_degree >= 0)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
 
@@ -198,9 +219,10 @@ def main():
                        "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                         "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if traffic else None,
                          "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch)},
-            "phase_ms_per_launch": {ph: round(times[ph][0] / max(times[ph][1], 1), 5) for ph in phases},
+            "phase_ms_per_launch": {ph: round(probe[ph][0] / max(probe[ph][1], 1), 5) for ph in PHASES},
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
         }

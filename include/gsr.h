@@ -131,6 +131,9 @@ int gsr_abi_version(void);
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
  * "render_bwd", "gauss_bwd".  gsr_profile_read synchronises on the recorded events. */
 int gsr_profile_enable(int on);
+/* Restrict event recording to a comma-separated list of phases (NULL or "" = every phase), so a
+ * timed region can carry the events of one kernel only.  Host-side timers are unaffected. */
+int gsr_profile_select(const char *phases);
 int gsr_profile_reset(void);
 int gsr_profile_read(const char *phase, double *total_ms, int *count);
 

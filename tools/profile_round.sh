@@ -1,7 +1,9 @@
 #!/bin/bash
 # Profile bench.py with rocprofv3 on the GPU box: kernel trace + stats, then the HBM counters in
-# two separate PMC passes (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950).
+# two separate PMC passes (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950).  Same bench
+# arguments in every pass, so the per-launch averages describe the command bench.py reports on.
 # usage (on the box, from the repo root): bash tools/profile_round.sh <tag> [bench args...]
+# outputs: gpurun_out/prof_<tag>/{trace,fetch,write}/ raw CSV, trace_summary.txt, hbm_pmc.json
 set -u
 tag=${1:-r01}; shift || true
 R=$(pwd)
@@ -9,11 +11,16 @@ O=$R/gpurun_out/prof_$tag
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -- \
-    python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline "$@" > "$O/trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
+    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 echo "trace ok"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/fetch" -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$O/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 2; }
+    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 2; }
 echo "fetch ok"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/write" -- \
-    python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 3; }
+    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 3; }
 echo "write ok"
+cd "$R"
+python3 tools/rocprof_summary.py trace "$O/trace" --last 20 --out "$O/trace_summary.json" > "$O/trace_summary.txt"
+python3 tools/rocprof_summary.py pmc "$O/fetch" "$O/write" --out "$O/hbm_pmc.json" > "$O/hbm_pmc.txt"
+cp "$O"/trace/*/*_kernel_stats.csv "$O/kernel_stats.csv" 2>/dev/null || true
+echo "summaries ok"

@@ -1,7 +1,8 @@
 """Summarise rocprofv3 CSV output into per-kernel tables (profiles/ evidence for bench.py).
 
 Usage:
-  python tools/rocprof_summary.py trace  <dir>            -> per-kernel calls / avg / total us
+  python tools/rocprof_summary.py trace  <dir> [--last N] [--out x.json]
+        -> per-kernel calls / avg / total us (+ average of the last N launches = bench's timed steps)
   python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> [--out profiles/x.json]
         -> per-kernel avg FETCH_SIZE / WRITE_SIZE per launch and corrected HBM bytes
 
@@ -31,11 +32,15 @@ def _rows(d, pattern):
             yield from csv.DictReader(fh)
 
 
-def trace(d):
+def trace(d, last=0):
     acc = defaultdict(list)
-    for r in _rows(d, "*kernel_trace.csv"):
+    rows = sorted(_rows(d, "*kernel_trace.csv"), key=lambda r: int(r["Start_Timestamp"]))
+    for r in rows:
         acc[_short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = {k: {"calls": len(v), "avg_us": sum(v) / len(v), "total_us": sum(v)} for k, v in acc.items()}
+    if last:  # launches of bench.py's timed region (the last `last` calls of a once-per-step kernel)
+        for k, v in acc.items():
+            out[k]["timed_avg_us"] = sum(v[-last:]) / len(v[-last:])
     return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_us"]))
 
 
@@ -60,10 +65,12 @@ def pmc(fetch_dir, write_dir):
 def main():
     mode = sys.argv[1]
     if mode == "trace":
-        t = trace(sys.argv[2])
-        print(f"{'kernel':<28}{'calls':>8}{'avg_us':>12}{'total_us':>14}")
+        last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 0
+        t = trace(sys.argv[2], last)
+        print(f"{'kernel':<28}{'calls':>8}{'avg_us':>12}{'total_us':>14}" + (f"{'last%d_avg_us' % last:>16}" if last else ""))
         for k, v in t.items():
-            print(f"{k:<28}{v['calls']:>8}{v['avg_us']:>12.2f}{v['total_us']:>14.1f}")
+            print(f"{k:<28}{v['calls']:>8}{v['avg_us']:>12.2f}{v['total_us']:>14.1f}"
+                  + (f"{v['timed_avg_us']:>16.2f}" if last else ""))
         if "--out" in sys.argv:
             json.dump(t, open(sys.argv[sys.argv.index("--out") + 1], "w"), indent=1)
     elif mode == "pmc":
