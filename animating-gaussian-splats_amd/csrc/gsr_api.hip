@@ -114,6 +114,8 @@ int check_common(const gsr_camera *cam, const gsr_gaussians *g, bool need_opacit
         return fail(GSR_ERR_ARG, "image size must be positive (got %dx%d)", cam->image_width, cam->image_height);
     const int gx = div_up(cam->image_width, kTileW), gy = div_up(cam->image_height, kTileH);
     if (gx > 65535 || gy > 65535) return fail(GSR_ERR_UNSUPPORTED, "tile grid too large");
+    if (g->activations & ~(GSR_ACT_SIGMOID_OPACITY | GSR_ACT_EXP_SCALES | GSR_ACT_NORMALIZE_ROTATIONS))
+        return fail(GSR_ERR_ARG, "unknown activation bits 0x%x", g->activations);
     if (g->P == 0) return GSR_OK;
     if (!g->means3D || (need_opacity && !g->opacities))
         return fail(GSR_ERR_ARG, "means3D and opacities are required");
@@ -135,6 +137,7 @@ void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
     a.W = cam->image_width; a.H = cam->image_height;
     a.gx = div_up(a.W, kTileW); a.gy = div_up(a.H, kTileH);
     a.scale_modifier = g->scale_modifier;
+    a.act = g->activations;
     a.tan_fovx = cam->tan_fovx; a.tan_fovy = cam->tan_fovy;
     a.focal_y = a.H / (2.0f * a.tan_fovy);
     a.focal_x = a.W / (2.0f * a.tan_fovx);
@@ -281,6 +284,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     BwdArgs a;
     memset(&a, 0, sizeof(a));
     a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
+    a.act = f.act;
     a.scale_modifier = f.scale_modifier; a.tan_fovx = f.tan_fovx; a.tan_fovy = f.tan_fovy;
     a.focal_x = f.focal_x; a.focal_y = f.focal_y;
     a.means3D = f.means3D; a.scales = f.scales; a.rotations = f.rotations; a.shs = f.shs;

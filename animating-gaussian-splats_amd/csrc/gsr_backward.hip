@@ -316,7 +316,7 @@ __device__ inline void gauss_bwd_one(
     const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drot, float *s_row) {
+    float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec) {
     if (!(radii[i] > 0)) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -347,7 +347,13 @@ __device__ inline void gauss_bwd_one(
         acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc.x;
     }
     dL_dmeans2D[3 * i] = acc[0]; dL_dmeans2D[3 * i + 1] = acc[1]; dL_dmeans2D[3 * i + 2] = 0.f;
-    dL_dopacity[i] = acc[5];
+    // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
+    if (act & GSR_ACT_SIGMOID_OPACITY) {
+        const float o = rec[(size_t)kRecF4 * i + 1].y;
+        dL_dopacity[i] = acc[5] * ((1.f - o) * o);
+    } else {
+        dL_dopacity[i] = acc[5];
+    }
     dL_dcolors[3 * i] = acc[6]; dL_dcolors[3 * i + 1] = acc[7]; dL_dcolors[3 * i + 2] = acc[8];
     const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
 
@@ -358,12 +364,15 @@ __device__ inline void gauss_bwd_one(
     float c3[6];
     float3 s3 = make_float3(0, 0, 0);
     float4 q = make_float4(0, 0, 0, 0);
+    float qn = 0.f;
     if (cov3D_precomp) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = cov3D_precomp[6 * i + k];
     } else {
         s3 = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
         q = make_float4(rotations[4 * i], rotations[4 * i + 1], rotations[4 * i + 2], rotations[4 * i + 3]);
+        if (act & GSR_ACT_EXP_SCALES) s3 = act_exp3(s3);
+        if (act & GSR_ACT_NORMALIZE_ROTATIONS) { qn = quat_norm(q); q = act_normalize(q, qn); }
         cov3d_from_scale_rot(s3, scale_modifier, q, c3);
     }
     // ---- computeCov2DCUDA ----
@@ -462,6 +471,8 @@ __device__ inline void gauss_bwd_one(
     if (scales && !cov3D_precomp) {
         float3 ds; float4 dr;
         cov3d_backward(s3, scale_modifier, q, dcov, ds, dr);
+        if (act & GSR_ACT_EXP_SCALES) { ds.x *= s3.x; ds.y *= s3.y; ds.z *= s3.z; }
+        if (act & GSR_ACT_NORMALIZE_ROTATIONS) dr = act_normalize_bwd(q, qn, dr);
         dL_dscales[3 * i] = ds.x; dL_dscales[3 * i + 1] = ds.y; dL_dscales[3 * i + 2] = ds.z;
         dL_drot[4 * i] = dr.x; dL_drot[4 * i + 1] = dr.y; dL_drot[4 * i + 2] = dr.z; dL_drot[4 * i + 3] = dr.w;
     } else {
@@ -481,7 +492,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drot) {
+    float *__restrict__ dL_drot, int act, const float4 *__restrict__ rec) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
@@ -498,7 +509,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     if (i < P) gauss_bwd_one<MC>(i, D, M, W, H, scale_modifier, tan_fovx, tan_fovy, h_x, h_y, means3D,
                                  scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos,
                                  radii, goff, part, dL_dmeans2D, dL_dcolors, dL_dopacity,
-                                 dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS);
+                                 dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
+                                 act, rec);
     if (MC > 0) {  // coalesced store of the dL/dSH rows
         __syncthreads();
         float *dst = dL_dsh + (size_t)i0 * RL;
@@ -528,7 +540,7 @@ static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
         a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
         a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
         a.radii, a.goff, a.part, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
-        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot);
+        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot, a.act, a.rec);
 }
 
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {

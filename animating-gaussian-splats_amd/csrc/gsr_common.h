@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/gsr.h"  // gsr_activation bits
+
 namespace gsr {
 
 constexpr int kTileW = 16;  // 16x16 pixel tiles (upstream BLOCK_X/BLOCK_Y)
@@ -194,6 +196,23 @@ __device__ inline void cov3d_from_scale_rot(float3 s3, float mod, float4 q, floa
     cov[0] = GM(Sig, 0, 0); cov[1] = GM(Sig, 0, 1); cov[2] = GM(Sig, 0, 2);
     cov[3] = GM(Sig, 1, 1); cov[4] = GM(Sig, 1, 2); cov[5] = GM(Sig, 2, 2);
 }
+
+// ---- fused parameter activations (shared.py:33-41; gsr_activation bits) ----
+// torch.nn.functional.normalize(q, dim=-1, eps=1e-12) = q / max(|q|, eps), |q| = sqrt(sum q_k^2)
+__device__ inline float quat_norm(float4 q) { return sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w); }
+__device__ inline float4 act_normalize(float4 q, float n) {
+    const float c = fmaxf(n, 1e-12f);
+    return make_float4(q.x / c, q.y / c, q.z / c, q.w / c);
+}
+// d/dq_raw of q_raw / max(|q_raw|, eps): (g - qhat (qhat . g)) / |q| when |q| > eps, else g / eps
+__device__ inline float4 act_normalize_bwd(float4 qhat, float n, float4 g) {
+    if (!(n > 1e-12f)) return make_float4(g.x / 1e-12f, g.y / 1e-12f, g.z / 1e-12f, g.w / 1e-12f);
+    const float d = qhat.x * g.x + qhat.y * g.y + qhat.z * g.z + qhat.w * g.w;
+    return make_float4((g.x - qhat.x * d) / n, (g.y - qhat.y * d) / n, (g.z - qhat.z * d) / n,
+                       (g.w - qhat.w * d) / n);
+}
+__device__ inline float act_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ inline float3 act_exp3(float3 s) { return make_float3(expf(s.x), expf(s.y), expf(s.z)); }
 
 __device__ inline float3 cov2d(float3 mean, float fx, float fy, float tfx, float tfy, const float *c3,
                                const float *vm) {

@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     const float *__restrict__ projmatrix, const float *__restrict__ campos, int W, int H,
     float tan_fovx, float tan_fovy, float focal_x, float focal_y, int gx, int gy,
     int *__restrict__ radii, float *__restrict__ depth_out, float4 *__restrict__ rec_out,
-    uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out) {
+    uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out, int act) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
@@ -63,9 +63,11 @@ __global__ __launch_bounds__(256) void k_preprocess(
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = cov3D_precomp[6 * i + k];
     } else {
-        const float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-        const float4 q = make_float4(rotations[4 * i], rotations[4 * i + 1], rotations[4 * i + 2],
-                                     rotations[4 * i + 3]);
+        float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
+        float4 q = make_float4(rotations[4 * i], rotations[4 * i + 1], rotations[4 * i + 2],
+                               rotations[4 * i + 3]);
+        if (act & GSR_ACT_EXP_SCALES) s = act_exp3(s);
+        if (act & GSR_ACT_NORMALIZE_ROTATIONS) q = act_normalize(q, quat_norm(q));
         cov3d_from_scale_rot(s, scale_modifier, q, c3);
     }
     const float3 cv = cov2d(p, focal_x, focal_y, tan_fovx, tan_fovy, c3, vm);
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
-    const float o = opacities[i];
+    const float o = (act & GSR_ACT_SIGMOID_OPACITY) ? act_sigmoid(opacities[i]) : opacities[i];
     const float ca = cv.z * det_inv, cb = -cv.y * det_inv, cc = cv.x * det_inv;
     const float tau2 = o >= 1.0f / 255.0f ? 2.f * log2f(255.f * o) : -1.f;
     float4 *r = rec_out + (size_t)kRecF4 * i;
@@ -559,7 +561,7 @@ static void preprocess_mc(const FwdArgs &a, hipStream_t s) {
     k_preprocess<MC><<<div_up(a.P, kShBlock), kShBlock, sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0), s>>>(
         a.P, a.D, a.M, a.means3D, a.scales, a.scale_modifier, a.rotations, a.opacities, a.shs,
         a.colors_precomp, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
-        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles);
+        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles, a.act);
 }
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {

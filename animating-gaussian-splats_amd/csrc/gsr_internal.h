@@ -11,7 +11,7 @@ constexpr int kMaxLdsTiles = 16384;
 
 struct FwdArgs {
     // inputs
-    int P, D, M, W, H, gx, gy;
+    int P, D, M, W, H, gx, gy, act;
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;
@@ -28,7 +28,7 @@ struct FwdArgs {
 };
 
 struct BwdArgs {
-    int P, D, M, W, H, gx, gy, K;
+    int P, D, M, W, H, gx, gy, K, act;
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *means3D, *scales, *rotations, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;

@@ -45,7 +45,8 @@ class _Gaussians(ctypes.Structure):
                 ("scale_modifier", ctypes.c_float), ("means3D", ctypes.c_void_p),
                 ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
                 ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
-                ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p)]
+                ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
+                ("activations", ctypes.c_int)]
 
 
 class _Grads(ctypes.Structure):
@@ -94,8 +95,15 @@ def load_library():
     L.gsr_profile_read.restype = i
     L.gsr_buffer_offsets.restype = i
     L.gsr_buffer_offsets.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_size_t), i]
+    if L.gsr_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libgsr.so ABI {L.gsr_abi_version()} != binding ABI {ABI_VERSION}: rebuild it")
     _lib = L
     return L
+
+
+ABI_VERSION = 2  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
+ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
 
 def _check(rc):
@@ -153,7 +161,8 @@ def _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_widt
                    _ptr(bg_), int(bool(prefiltered)))
 
 
-def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier, cov3D, keep):
+def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier, cov3D, keep,
+               activations=0):
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     P = means3D.size(0)
@@ -162,23 +171,26 @@ def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_mo
     means3D, sh, colors, opacity, scales, rotations, cov3D = ts
     M = sh.size(1) if sh is not None and sh.numel() else 0
     return _Gaussians(P, int(degree), M, float(scale_modifier), _ptr(means3D), _ptr(sh), _ptr(colors),
-                      _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(cov3D)), P, M
+                      _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(cov3D),
+                      int(activations)), P, M
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
-                        image_width, sh, degree, campos, prefiltered, debug=False):
+                        image_width, sh, degree, campos, prefiltered, debug=False, activations=0):
+    """``activations`` (ACT_* bits): opacity / scales / rotations hold the raw parameters of
+    shared.py:29-42 and are activated inside the kernels (0 = the reference's interface)."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
-                         cov3D_precomp, keep)
+                         cov3D_precomp, keep, activations)
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, campos,
                   background, prefiltered, keep)
     dev = means3D.device
     H, W = int(image_height), int(image_width)
     color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
     depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
-    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    radii = torch.empty((P,), dtype=torch.int32, device=dev)  # preprocess writes every entry
     alloc = _Allocator(dev)
     nr = ctypes.c_int(0)
     _check(L.gsr_forward(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
@@ -191,11 +203,12 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations,
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
-                                 binningBuffer, imageBuffer, debug=False, dL_dout_depth=None):
+                                 binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
+                                 activations=0):
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
-                         rotations, scale_modifier, cov3D_precomp, keep)
+                         rotations, scale_modifier, cov3D_precomp, keep, activations)
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device

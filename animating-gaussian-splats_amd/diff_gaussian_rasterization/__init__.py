@@ -19,7 +19,8 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
+           "rasterize_parameters"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -58,10 +59,13 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the unused depth output
         return color, radii, depth
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, grad_depth):
+        if grad_out_color is None:  # only depth was used: it carries no gradient (-w-depth)
+            return (None,) * 9
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
          binningBuffer, imgBuffer) = ctx.saved_tensors
@@ -107,3 +111,64 @@ class GaussianRasterizer(nn.Module):
             cov3D_precomp = empty
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales,
                                    rotations, cov3D_precomp, rs)
+
+
+def rasterize_parameters(params, raster_settings, means2D=None, shs=None):
+    """Fused ``create_render_arguments`` (shared.py:29-42) + ``GaussianRasterizer`` call
+    (train.py:359-361, densify.py:124-126): the caller's normalize / sigmoid / exp activations run
+    inside the preprocess kernel and their derivatives inside the per-Gaussian backward kernel, so
+    no activated copies or autograd nodes are created and gradients land directly on
+    ``params["means"]``, ``params["rotation_quaternions"]``, ``params["opacity_logits"]``,
+    ``params["log_scales"]`` and ``params["colors"]`` (or ``shs`` when given).
+
+    ``means2D``: optional (P, 3) tensor requiring grad; it receives the screen-space (NDC) gradient
+    that the reference reads through ``means2D.retain_grad()`` (densify.py:119, external.py:117).
+    Returns ``(color (3,H,W), radii (P,), depth (1,H,W))`` like ``GaussianRasterizer``.
+    """
+    means = params["means"]
+    if means2D is None:
+        means2D = torch.empty(0, device=means.device)
+    colors = params["colors"] if shs is None else torch.empty(0, device=means.device)
+    if shs is None:
+        shs = torch.empty(0, device=means.device)
+    return _RasterizeGaussianParameters.apply(means, means2D, shs, colors, params["opacity_logits"],
+                                              params["log_scales"], params["rotation_quaternions"],
+                                              raster_settings)
+
+
+class _RasterizeGaussianParameters(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means, means2D, sh, colors, opacity_logits, log_scales, quaternions, raster_settings):
+        rs = raster_settings
+        empty = torch.empty(0, device=means.device)
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians(
+            rs.bg, means, colors, opacity_logits, log_scales, quaternions, rs.scale_modifier, empty,
+            rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
+            rs.sh_degree, rs.campos, rs.prefiltered, activations=_C.ACT_ALL)
+        ctx.raster_settings = rs
+        ctx.num_rendered = num_rendered
+        ctx.opacity_shape = opacity_logits.shape
+        ctx.save_for_backward(colors, means, log_scales, quaternions, radii, sh, geomBuffer,
+                              binningBuffer, imgBuffer)
+        ctx.mark_non_differentiable(radii)
+        ctx.set_materialize_grads(False)
+        return color, radii, depth
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii, _grad_depth):
+        if grad_out_color is None:
+            return (None,) * 8
+        rs = ctx.raster_settings
+        colors, means, log_scales, quaternions, radii, sh, geomBuffer, binningBuffer, imgBuffer = \
+            ctx.saved_tensors
+        empty = torch.empty(0, device=means.device)
+        (g_means2D, g_colors, g_opacity, g_means, _g_cov3D, g_sh, g_scales, g_rot) = \
+            _C.rasterize_gaussians_backward(
+                rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
+                rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
+                activations=_C.ACT_ALL)
+        need = ctx.needs_input_grad
+        return (g_means, g_means2D if need[1] else None, g_sh if sh.numel() else None,
+                g_colors if colors.numel() else None, g_opacity.view(ctx.opacity_shape), g_scales, g_rot,
+                None)

@@ -4,10 +4,15 @@ Metric: Msplats/s = P x views / wall-time(forward + backward) / 1e6, P counted p
 (SURVEY.md 8(d)).  Workload (BASELINE.json configs[2], the 1-GPU config the metric is quoted on):
 1M synthetic Gaussians, SH degree 3, 1920x1080, f = 1600, views from the 27-camera rig of
 configs[3] (heights {-0.8, 0, 0.8} x yaws {0, 40, ..., 320}).  One step = every rank renders
-``--views-per-rank`` views through the drop-in ``GaussianRasterizer`` (activations of
-shared.py:29-42 included), backpropagates a fixed upstream dL/dcolor into the leaf parameters
-(gradients accumulate over the rank's views, as train.py sums view losses), and for N > 1
-all-reduces (SUM) the parameter gradients over RCCL.  Inputs are resident in HBM before timing.
+``--views-per-rank`` views through the drop-in ``GaussianRasterizer`` on the render arguments of
+shared.py:29-42 (activated once, before timing, and held as leaf tensors: SURVEY.md 8(d) times the
+rasterizer's forward + backward), backpropagates a fixed upstream dL/dcolor into them (gradients
+accumulate over the rank's views, as train.py sums view losses), and for N > 1 all-reduces (SUM)
+the gradients over RCCL.  Inputs are resident in HBM before timing.
+
+Also reported (untimed for `value`, ``call_site``): ms per view of train.py's whole render call
+site, (a) the reference's way -- torch activations + their autograd + the drop-in -- and (b) the
+fused ``rasterize_parameters`` path (activations inside the kernels).
 
 N > 1: launched by torch.distributed.run, one process per GPU; the step's N * V rig cameras
 (step * N * V + k) mod 27 are sharded round-robin over ranks (splat_dp.shard_views; camera data
@@ -82,6 +87,8 @@ def main():
     ap.add_argument("--views-per-rank", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--call-site-steps", type=int, default=10,
+                    help="steps timed for each train.py call-site variant (0 = skip)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="untimed steps with events on every phase (per-kernel breakdown)")
     args = ap.parse_args()
@@ -111,21 +118,54 @@ def main():
     V = args.views_per_rank
 
     import splat_dp
-    reducer = splat_dp.GradAllReduce(params.values()) if dist is not None else None
+    from diff_gaussian_rasterization import rasterize_parameters
+    # the rasterizer's inputs: render arguments of shared.py:29-42, activated once, as leaves
+    with torch.no_grad():
+        act = S.activated_inputs(params, cfg.sh_degree)
+    if cfg.sh_degree >= 0:
+        act.pop("colors_precomp")
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
+    reducer = splat_dp.GradAllReduce([v for k, v in leaves.items() if k != "means2D"]) \
+        if dist is not None else None
+
+    def views_of(it):
+        # rank r renders its round-robin share of this step's world * V rig cameras
+        return splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)],
+                                    rank, world)
 
     def step(it):
-        # rank r renders its round-robin share of this step's world * V rig cameras
-        step_cams = [(it * world * V + k) % len(cams) for k in range(world * V)]
-        for ci in splat_dp.shard_views(step_cams, rank, world):
+        for ci in views_of(it):
+            img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
+            img.backward(dl)
+        if reducer is not None:
+            reducer()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
+        for p in leaves.values():
+            p.grad = None
+
+    def step_reference_call_site(it):  # train.py: create_render_arguments + Renderer + backward
+        for ci in views_of(it):
             a = S.activated_inputs(params, cfg.sh_degree)
             if cfg.sh_degree >= 0:
                 a.pop("colors_precomp")
             img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**a)
             img.backward(dl)
-        if reducer is not None:
-            reducer()  # one flat-bucket all-reduce (SUM) of every parameter gradient over RCCL
         for p in params.values():
             p.grad = None
+
+    def step_fused_call_site(it):  # the same through rasterize_parameters (fused activations)
+        for ci in views_of(it):
+            img, _radii, _depth = rasterize_parameters(params, cams[ci], shs=params.get("shs"))
+            img.backward(dl)
+        for p in params.values():
+            p.grad = None
+
+    def time_steps(fn, n, first):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for it in range(n):
+            fn(first + it)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / n * 1e3
 
     for it in range(args.warmup):
         step(it)
@@ -164,6 +204,17 @@ def main():
     # dominant kernel's device time inside the timed region (HIP events on its launch stream)
     tot_ms, cnt = _C.profile_read(dom)
     _C.profile_select(None)
+    call_site = None
+    if args.call_site_steps > 0:
+        first = args.warmup + args.probe_steps
+        per_view = len(views_of(first))
+        time_steps(step_reference_call_site, 3, first)  # warm each path's kernels and allocations
+        ref_ms = time_steps(step_reference_call_site, args.call_site_steps, first)
+        time_steps(step_fused_call_site, 3, first)
+        fused_ms = time_steps(step_fused_call_site, args.call_site_steps, first)
+        call_site = {"reference_activations_ms_per_view": round(ref_ms / per_view, 4),
+                     "fused_activations_ms_per_view": round(fused_ms / per_view, 4),
+                     "steps": args.call_site_steps}
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
     import splat_dp
@@ -225,6 +276,7 @@ def main():
             "phase_ms_per_launch": {ph: round(probe[ph][0] / max(probe[ph][1], 1), 5) for ph in PHASES},
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
+            "call_site": call_site,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 1
+#define GSR_ABI_VERSION 2
 
 enum gsr_status {
     GSR_OK = 0,
@@ -65,7 +65,21 @@ typedef struct gsr_camera {
     int prefiltered;         /* accepted; the near-plane cull is applied either way */
 } gsr_camera;
 
-/* Per-Gaussian inputs: the render arguments of shared.py:29-42 (already activated). */
+/* Fused parameter activations (bit mask, gsr_gaussians.activations).  The reference's caller
+ * activates the raw parameters before every render (shared.py:33-41: rotations =
+ * normalize(rotation_quaternions), opacities = sigmoid(opacity_logits), scales = exp(log_scales));
+ * with a bit set the corresponding pointer holds the RAW parameter, the kernels apply the
+ * activation on load, and gsr_backward returns the gradient with respect to the raw parameter
+ * (the chain rule of torch's normalize(eps = 1e-12) / sigmoid / exp).  0 = inputs already activated,
+ * exactly the reference's _C interface. */
+enum gsr_activation {
+    GSR_ACT_NONE = 0,
+    GSR_ACT_SIGMOID_OPACITY = 1,
+    GSR_ACT_EXP_SCALES = 2,
+    GSR_ACT_NORMALIZE_ROTATIONS = 4
+};
+
+/* Per-Gaussian inputs: the render arguments of shared.py:29-42 (activated unless `activations`). */
 typedef struct gsr_gaussians {
     int P;                       /* number of Gaussians (>= 0) */
     int sh_degree;               /* active SH degree D (0..3) */
@@ -78,6 +92,7 @@ typedef struct gsr_gaussians {
     const float *scales;         /* (P,3)   or NULL -- scales+rotations, or cov3D_precomp */
     const float *rotations;      /* (P,4)   or NULL */
     const float *cov3D_precomp;  /* (P,6)   or NULL */
+    int activations;             /* gsr_activation bit mask (ABI >= 2); 0 = activated inputs */
 } gsr_gaussians;
 
 /* Gradient outputs of gsr_backward, in the order _C.rasterize_gaussians_backward returns them.

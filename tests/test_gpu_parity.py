@@ -281,3 +281,51 @@ def test_rasterizer_module_autograd(cuda):
     vis = GaussianRasterizer(raster_settings=rs).markVisible(params["means"].detach())
     np.testing.assert_array_equal(_np(vis), O.mark_visible(p["means"].cpu().numpy(), rs.viewmatrix.cpu(),
                                                            rs.projmatrix.cpu()))
+
+
+@pytest.mark.parametrize("case", ["c1", "sh3", "ragged_bg"])
+def test_fused_parameters_parity(case, cuda):
+    """rasterize_parameters (normalize / sigmoid / exp of shared.py:33-41 inside the kernels) against
+    the oracle fed with torch's own CPU activations, its gradients chained back to the raw
+    parameters by torch autograd on the CPU (the reference's caller path, end to end)."""
+    from diff_gaussian_rasterization import rasterize_parameters
+    P, W, H, f, s0, shd, extra = CASES[case]
+    p = S.synthetic_cloud(P, s0, sh_degree=shd, seed=3, device="cpu")
+    g = torch.Generator().manual_seed(17)  # un-normalised raw quaternions: exercise normalize's chain rule
+    p["rotation_quaternions"] = p["rotation_quaternions"] * (0.5 + 1.5 * torch.rand(P, 1, generator=g))
+    raw = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    act = S.activated_inputs(raw, shd)
+    a = {k: v.detach() for k, v in act.items() if isinstance(v, torch.Tensor) and k != "means2D"}
+    if shd >= 0:
+        a.pop("colors_precomp", None)
+    rs = S.render_settings(W, H, S.intrinsics(f, W, H), S.look_at(extra.get("yaw", 0.0), 0.0, 4.0),
+                           device="cpu", sh_degree=max(shd, 0))
+    rs = rs._replace(bg=torch.tensor(extra.get("bg", (0.0, 0.0, 0.0)), dtype=torch.float32))
+    st = _ora_forward(a, rs)
+    dl = S.upstream_grad(H, W, device="cpu")
+    gref = O.backward(st, dl.numpy())
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(gref[k]))  # noqa: E731
+    torch.autograd.backward([act["opacities"], act["scales"], act["rotations"]],
+                            [t("opacities").view_as(act["opacities"]), t("scales"), t("rotations")])
+
+    gp = {k: v.detach().to(cuda).requires_grad_(True) for k, v in p.items()}
+    means2D = torch.zeros(P, 3, device=cuda, requires_grad=True)
+    rsg = rs._replace(bg=rs.bg.to(cuda), viewmatrix=rs.viewmatrix.to(cuda),
+                      projmatrix=rs.projmatrix.to(cuda), campos=rs.campos.to(cuda))
+    color, radii, depth = rasterize_parameters(gp, rsg, means2D=means2D,
+                                               shs=gp["shs"] if shd >= 0 else None)
+    (color * dl.to(cuda)).sum().backward()
+    same_r = (_np(radii) == st["radii"]).mean()
+    assert same_r >= 1 - 1e-3, f"radii differ on {1 - same_r:.2e} of Gaussians"
+    _close("fused.color", _np(color), st["color"], atol_frac=1e-6, max_bad_frac=1e-4)
+    _close("fused.depth", _np(depth), st["depth"], atol_frac=1e-6, max_bad_frac=1e-4)
+    _close("fused.means2D", _np(means2D.grad), gref["means2D"], max_bad_frac=1e-3)
+    _close("fused.means", _np(gp["means"].grad), gref["means3D"], max_bad_frac=1e-3)
+    if shd >= 0:
+        _close("fused.shs", _np(gp["shs"].grad), gref["sh"], max_bad_frac=1e-3)
+        assert gp["colors"].grad is None
+    else:
+        _close("fused.colors", _np(gp["colors"].grad), gref["colors"], max_bad_frac=1e-3)
+    for k in ("opacity_logits", "log_scales", "rotation_quaternions"):
+        assert gp[k].grad.shape == raw[k].shape
+        _close("fused." + k, _np(gp[k].grad), raw[k].grad.numpy(), max_bad_frac=1e-3)
