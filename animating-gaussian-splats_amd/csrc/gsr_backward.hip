@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const int py0 = ty * kTileH + (lane >> 4);
     const float pfx = (float)px;
     const float tx0 = (float)(tx * kTileW), ty0 = (float)(ty * kTileH);
-    const float tx1 = tx0 + (kTileW - 1), ty1 = ty0 + (kTileH - 1);
+    const float tx1 = tx0 + (kTileW - 1);
     const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
     const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
     for (int p = maxc + lane; p < n; p += 64) {  // slots nobody reached: zero records
@@ -73,11 +73,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     }
     const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-    // Per pixel state of the reverse walk.  The reference keeps accum_rec and last_color per channel,
-    // but dL/dalpha only needs their projections on dL/dpixel, and the recurrence
-    // accum_rec = last_alpha * last_color + (1 - last_alpha) * accum_rec is linear, so AR = <accum_rec,
-    // dL/dpix> and LC = <last_color, dL/dpix> are carried as scalars (same value, fewer registers).
-    float Tt[4], tbg[4], dp0[4], dp1[4], dp2[4], AR[4], LC[4], la[4], pfy[4];
+    // Per pixel state of the reverse walk.  The reference keeps accum_rec and last_color per channel
+    // and folds the previous contributor into accum_rec when it meets the next one; dL/dalpha only
+    // needs the projection of accum_rec on dL/dpixel, and folding eagerly right after each
+    // contributor (AR <- AR + alpha (<c, dL/dpix> - AR)) gives the same value with the same
+    // rounding, while a non-contributing pair (alpha = 0) leaves it untouched without a select.
+    float Tt[4], tbg[4], dp0[4], dp1[4], dp2[4], AR[4], pfy[4];
     uint32_t lastc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -94,7 +95,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         float bd = 0;
         bd += bg0 * dp0[k]; bd += bg1 * dp1[k]; bd += bg2 * dp2[k];
         tbg[k] = -Tf * bd;  // background term of dL/dalpha: -T_final / (1 - alpha) * <bg, dL/dpix>
-        AR[k] = 0.f; LC[k] = 0.f; la[k] = 0.f;
+        AR[k] = 0.f;
     }
     const int row = lane >> 4;
     const int slot0123 = (row == 0) ? 0 : (row == 1) ? 2 : (row == 2) ? 1 : 3;  // wave_sum9 lane map
@@ -103,19 +104,24 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         const int cnt = end - start;
 #pragma unroll
         for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
-        // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile
+        // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile; a
+        // quarter whose pixels all precede this slot in the forward's order (p >= its max
+        // n_contrib) is skipped too
         uint32_t qmask = 0;
         float4 cj = make_float4(0.f, 0.f, 0.f, 0.f);  // exact conic of the Gaussian this lane staged
         uint32_t em = 0;                              // emission index of the pair this lane staged
         if (lane < cnt) {
-            const uint32_t g = point_list[rg.x + start + lane];
-            em = slot_emit[rg.x + start + lane];
+            const uint32_t p = (uint32_t)(start + lane);
+            const uint32_t g = point_list[rg.x + p];
+            em = slot_emit[rg.x + p];
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
             cj = rec[(size_t)kRecF4 * g + 3];
             s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
+            const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                if (!tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0 + 4 * k, tx1, ty0 + 4 * k + 3))
+                if (p < qmax[k] &&
+                    !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0 + 4 * k, tx1, ty0 + 4 * k + 3))
                     qmask |= 1u << k;
         }
         s_q[lane] = qmask;
@@ -125,42 +131,45 @@ __global__ __launch_bounds__(256) void k_render_bwd(
             const int j = 63 - __builtin_clzll(m);
             m &= ~(1ull << j);
             const uint32_t p = (uint32_t)(start + j);
-            const uint32_t qm = s_q[j];
+            const uint32_t qm = __builtin_amdgcn_readfirstlane(s_q[j]);  // wave-uniform quarter mask
             const float4 a = s_a[j], b = s_b[j], c = s_c[j];
-            float v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0, v5 = 0, v6 = 0, v7 = 0, v8 = 0;
+            const PairX x = pair_x(a, pfx);
+            // per-lane sums over this lane's pixels: S0 = sum G dL/dalpha, S1 = sum G dL/dalpha dy,
+            // S4 = sum G dL/dalpha dy^2, cs = sum alpha T dL/dpix (the lane's 4 pixels share dx)
+            float S0 = 0.f, S1 = 0.f, S4 = 0.f, cs0 = 0.f, cs1 = 0.f, cs2 = 0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
                 // branch-free: a non-contributing pixel gets alpha = 0, which makes every update an
-                // identity (r = 1, dch = 0) and the state selects keep the previous contributor
-                const Blend e = blend_eval(a, b, pfx, pfy[k]);
-                const bool ok = p < lastc[k] && blend_ok(e);
+                // identity (r = 1, AR unchanged, zero sums)
+                const float dy = a.y - pfy[k];
+                const float p2 = pair_power(x, b.x, dy);
+                const float G = __builtin_amdgcn_exp2f(p2);
+                const float alpha = fminf(0.99f, b.y * G);
+                const bool ok = p < lastc[k] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
                 any = any || ok;
-                const float al = ok ? e.alpha : 0.f;
+                const float al = ok ? alpha : 0.f;
                 const float r = __builtin_amdgcn_rcpf(1.f - al);
                 Tt[k] = Tt[k] * r;
-                const float dch = al * Tt[k];
                 const float cd = fmaf(c.z, dp2[k], fmaf(c.y, dp1[k], c.x * dp0[k]));  // <colour, dL/dpix>
-                AR[k] = ok ? fmaf(la[k], LC[k] - AR[k], AR[k]) : AR[k];
-                LC[k] = ok ? cd : LC[k];
-                la[k] = ok ? e.alpha : la[k];
-                float dLa = fmaf(r, tbg[k], (cd - AR[k]) * Tt[k]);
-                dLa = ok ? dLa : 0.f;
-                const float sG = b.y * dLa * e.G;  // dL/dG * G
-                const float t = sG * e.dx, u = sG * e.dy;
-                v0 += t;
-                v1 += u;
-                v2 = fmaf(t, e.dx, v2);
-                v3 = fmaf(t, e.dy, v3);
-                v4 = fmaf(u, e.dy, v4);
-                v5 = fmaf(e.G, dLa, v5);
-                v6 = fmaf(dch, dp0[k], v6);
-                v7 = fmaf(dch, dp1[k], v7);
-                v8 = fmaf(dch, dp2[k], v8);
+                const float diff = cd - AR[k];
+                const float dLa = fmaf(r, tbg[k], diff * Tt[k]);
+                AR[k] = fmaf(al, diff, AR[k]);
+                const float gd = ok ? G * dLa : 0.f;
+                const float u = gd * dy;
+                S0 += gd;
+                S1 += u;
+                S4 = fmaf(u, dy, S4);
+                const float dch = al * Tt[k];
+                cs0 = fmaf(dch, dp0[k], cs0);
+                cs1 = fmaf(dch, dp1[k], cs1);
+                cs2 = fmaf(dch, dp2[k], cs2);
             }
             if (__ballot(any)) {
-                const Sum9 sm = wave_sum9(v0, v1, v2, v3, v4, v5, v6, v7, v8);
+                // moments of sG = opacity * G * dL/dalpha: (dx, dy, dx^2, dx dy, dy^2)
+                const float v0 = (b.y * x.dx) * S0, v1 = b.y * S1;
+                const Sum9 sm = wave_sum9(v0, v1, x.dx * v0, x.dx * v1, b.y * S4, S0, cs0, cs1, cs2);
                 if ((lane & 15) == 0) {
                     s_out[j * kPartial + slot0123] = sm.r0123;
                     s_out[j * kPartial + 4 + slot0123] = sm.r4567;

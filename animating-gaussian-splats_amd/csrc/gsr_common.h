@@ -318,17 +318,32 @@ constexpr int kTilesPerBlock = 4;
 
 // Blend weight of one (pixel, Gaussian) pair, shared by the forward and backward kernels so that
 // both take identical decisions: power2 = power * log2(e) evaluated with FMAs, G = 2^power2.
+// Exponent of the Gaussian at a pixel, log2 units: p2 = A2 dx^2 + B2 dx dy + C2 dy^2 with the
+// record's pre-scaled conic.  Evaluated as P0 + dy (P1 + C2 dy), P0 = (A2 dx) dx, P1 = B2 dx, so
+// the backward (4 pixels of one column per lane) computes the dx-only part once per pair; forward
+// and backward use this exact operation sequence, hence bitwise-identical blend decisions.
+struct PairX { float dx, P0, P1; };
+__device__ inline PairX pair_x(float4 r0, float pfx) {
+    PairX x;
+    x.dx = r0.x - pfx;
+    x.P0 = (r0.z * x.dx) * x.dx;
+    x.P1 = r0.w * x.dx;
+    return x;
+}
+__device__ inline float pair_power(const PairX &x, float C2, float dy) { return fmaf(dy, fmaf(C2, dy, x.P1), x.P0); }
+
 struct Blend { float dx, dy, p2, G, alpha; };
 __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
     Blend e;
-    e.dx = r0.x - pfx;
+    const PairX x = pair_x(r0, pfx);
+    e.dx = x.dx;
     e.dy = r0.y - pfy;
-    e.p2 = fmaf(e.dx, fmaf(r0.z, e.dx, r0.w * e.dy), r1.x * e.dy * e.dy);
+    e.p2 = pair_power(x, r1.x, e.dy);
     e.G = __builtin_amdgcn_exp2f(e.p2);
     e.alpha = fminf(0.99f, r1.y * e.G);
     return e;
 }
-__device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }  // render kernels: 4 independent tiles (one wave64 each) per block
+__device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }
 
 // Make this wave's LDS writes visible to its own later LDS reads (waves of a render block work
 // on different tiles and never synchronise with each other).
