@@ -252,9 +252,8 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
     carve_binning(a, bin, (int)K);
     { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, (int)K, s)); }
-    uint32_t n_per_path[3];
-    for (int c = 0; c < 3; ++c) n_per_path[c] = __atomic_load_n(hw.h + 1 + c, __ATOMIC_ACQUIRE);
-    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_per_path, s)); }
+    const uint32_t n_long = __atomic_load_n(hw.h + 1, __ATOMIC_ACQUIRE);
+    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_long, s)); }
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     return GSR_OK;
 }

@@ -18,10 +18,9 @@ constexpr int kTileH = 16;
 constexpr int kTilePix = kTileW * kTileH;  // 256 = 4 wave64 per tile block
 constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic abc, dopacity, dcolour rgb
 constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
-constexpr int kRegSortShort = 512;   // lists up to this length: register sort, R <= 8 keys per lane
-constexpr int kRegSortMax = 1024;    // lists up to this length: register sort, R = 16
-// host-mapped words published by k_bin_scan: [0] = K (written last, release), [1..3] = number of
-// tiles on each sort path (short register / long register / LDS-global)
+constexpr int kFwdSortCap = 1024;  // lists up to this length are depth-sorted inside k_render_fwd
+// host-mapped words published by k_bin_scan: [0] = K (written last, release), [1] = number of
+// tiles longer than kFwdSortCap (sorted by k_tile_sort before the render), [2..3] unused
 constexpr int kHostWords = 4;
 
 __host__ __device__ inline int div_up(int a, int b) { return (a + b - 1) / b; }
@@ -79,7 +78,7 @@ struct ImageLayout {
         tile_cost = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter: sum of n_contrib
         tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
         tile_order_b = o; o = align256(o + sizeof(uint32_t) * T);    // backward dispatch order (LPT)
-        sort_lists = o;  o = align256(o + sizeof(uint32_t) * 3 * T);  // tiles per sort path (3 lists of T)
+        sort_lists = o;  o = align256(o + sizeof(uint32_t) * T);      // tiles longer than kFwdSortCap
         tile_count = o;  o = align256(o + sizeof(uint32_t) * T);
         tile_cursor = o; o = align256(o + sizeof(uint32_t) * T);
         block_sums = o;  o = align256(o + sizeof(uint32_t) * (NB + 1));

@@ -183,13 +183,12 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
         if (b < NB) block_off[b] = ex;
         carry2 += tot;
     }
-    // tiles per sort path (exact classes, so the host launches exactly the blocks each path needs)
+    // tiles too long for the in-render sort (k_tile_sort launches exactly one block per such tile)
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         const uint32_t n = tile_count[t];
         if (n == 0) continue;
-        const int c = n <= (uint32_t)kRegSortShort ? 0 : (n <= (uint32_t)kRegSortMax ? 1 : 2);
-        sort_lists[c * T + atomicAdd(&s_cls[c], 1u)] = (uint32_t)t;
+        if (n > (uint32_t)kFwdSortCap) sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -311,88 +310,91 @@ __device__ inline void bitonic_xlane(uint64_t (&k)[R], uint32_t (&v)[R], bool ta
     }
 }
 
-template <int R>
-__device__ inline void wave_bitonic_kv(uint64_t (&k)[R], uint32_t (&v)[R], int lane) {
-#pragma clang loop unroll(full)
-    for (int kk = 2; kk <= 64 * R; kk <<= 1) {
-#pragma clang loop unroll(full)
-        for (int j = kk >> 1; j > 0; j >>= 1) {
-            if (j < R) {
+// Stages j = J, J/2, ..., 1 (J < 64 R) of the bitonic merge of size KK, on the wave's elements
+// i = gbase + lane * R + r (ascending where (i & KK) == 0).
+template <int R, int KK, int J>
+__device__ inline void wave_merge_stages(uint64_t (&k)[R], uint32_t (&v)[R], int lane, uint32_t gbase) {
+    if constexpr (J > 0) {
+        if constexpr (J < R) {
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (r & j) continue;
-                    const int r2 = r | j;
-                    const bool asc = ((lane * R + r) & kk) == 0;
-                    if ((k[r] > k[r2]) == asc) {
-                        const uint64_t t = k[r]; k[r] = k[r2]; k[r2] = t;
-                        const uint32_t u = v[r]; v[r] = v[r2]; v[r2] = u;
-                    }
-                }
-            } else {
-                const int d = j / R;
-                const bool asc = ((lane * R) & kk) == 0;
-                const bool lower = (lane & d) == 0;
-                const bool take_min = lower == asc;
-                switch (d) {
-                    case 1: bitonic_xlane<R, 1>(k, v, take_min); break;
-                    case 2: bitonic_xlane<R, 2>(k, v, take_min); break;
-                    case 4: bitonic_xlane<R, 4>(k, v, take_min); break;
-                    case 8: bitonic_xlane<R, 8>(k, v, take_min); break;
-                    case 16: bitonic_xlane<R, 16>(k, v, take_min); break;
-                    default: bitonic_xlane<R, 32>(k, v, take_min); break;
+            for (int r = 0; r < R; ++r) {
+                if (r & J) continue;
+                const int r2 = r | J;
+                const bool asc = ((gbase + lane * R + r) & KK) == 0;
+                if ((k[r] > k[r2]) == asc) {
+                    const uint64_t t = k[r]; k[r] = k[r2]; k[r2] = t;
+                    const uint32_t u = v[r]; v[r] = v[r2]; v[r2] = u;
                 }
             }
+        } else {
+            constexpr int D = J / R;
+            const bool asc = ((gbase + lane * R) & KK) == 0;
+            const bool take_min = ((lane & D) == 0) == asc;
+            bitonic_xlane<R, D>(k, v, take_min);
         }
+        wave_merge_stages<R, KK, J / 2>(k, v, lane, gbase);
     }
 }
 
+// Full bitonic network over the wave's 64 R elements (merge sizes 2 .. 64 R); the last merge runs
+// descending when (gbase & 64 R) != 0, which is what the next cross-wave merge needs.
+template <int R, int KK>
+__device__ inline void wave_sort_stages(uint64_t (&k)[R], uint32_t (&v)[R], int lane, uint32_t gbase) {
+    if constexpr (KK <= 64 * R) {
+        wave_merge_stages<R, KK, KK / 2>(k, v, lane, gbase);
+        wave_sort_stages<R, 2 * KK>(k, v, lane, gbase);
+    }
+}
+
+// One cross-wave compare-exchange stage (distance J >= 64 R) of merge size KK through LDS.
 template <int R>
-__device__ inline void tile_sort_regs(int n, uint32_t start, const uint64_t *__restrict__ keys,
-                                      const uint32_t *__restrict__ vals, uint32_t *__restrict__ point_list,
-                                      uint32_t *__restrict__ slot_emit, int lane) {
+__device__ inline void block_xchg_stage(uint64_t (&k)[R], uint32_t (&v)[R], uint32_t ibase, int kk, int j,
+                                        uint64_t *s_key, uint32_t *s_val) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) { s_key[ibase + r] = k[r]; s_val[ibase + r] = v[r]; }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i = ibase + r, q = i ^ (uint32_t)j;
+        const uint64_t pk = s_key[q];
+        const uint32_t pv = s_val[q];
+        const bool take_min = ((i & j) == 0) == ((i & kk) == 0);
+        const bool mine = (k[r] < pk) == take_min;
+        k[r] = mine ? k[r] : pk;
+        v[r] = mine ? v[r] : pv;
+    }
+    __syncthreads();
+}
+
+// Sort one tile's n <= 256 R (key, emission) pairs with the block's 4 waves: each wave sorts its
+// 64 R-element segment in registers (DPP / swizzle / permlane exchanges), then the two cross-wave
+// merge levels exchange through LDS and finish in registers.  Leaves the sorted keys in s_key[0, n)
+// and emissions in s_val[0, n).  Keys are (depth_bits << 32 | index), unique inside a tile.
+template <int R>
+__device__ inline void block_sort_tile(int n, uint32_t start, const uint64_t *__restrict__ keys,
+                                       const uint32_t *__restrict__ vals, uint64_t *s_key, uint32_t *s_val) {
+    constexpr int SEG = 64 * R;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t gbase = (uint32_t)(w * SEG), ibase = gbase + lane * R;
     uint64_t k[R];
     uint32_t v[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int i = lane * R + r;
+        const int i = (int)ibase + r;
         k[r] = i < n ? keys[start + i] : ~0ull;  // +inf padding sorts to the end
         v[r] = i < n ? vals[start + i] : 0u;
     }
-    wave_bitonic_kv<R>(k, v, lane);
+    wave_sort_stages<R, 2>(k, v, lane, gbase);
+    // merge of size 2 SEG: one LDS stage (j = SEG), then j < SEG in registers
+    block_xchg_stage<R>(k, v, ibase, 2 * SEG, SEG, s_key, s_val);
+    wave_merge_stages<R, 2 * SEG, SEG / 2>(k, v, lane, gbase);
+    // merge of size 4 SEG (the whole block): j = 2 SEG and SEG through LDS, then registers
+    block_xchg_stage<R>(k, v, ibase, 4 * SEG, 2 * SEG, s_key, s_val);
+    block_xchg_stage<R>(k, v, ibase, 4 * SEG, SEG, s_key, s_val);
+    wave_merge_stages<R, 4 * SEG, SEG / 2>(k, v, lane, gbase);
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int i = lane * R + r;
-        if (i < n) {
-            point_list[start + i] = (uint32_t)k[r];
-            slot_emit[start + i] = v[r];
-        }
-    }
-}
-
-// One wave per tile (4 tiles per block, no barriers), lists sorted entirely in registers.
-// LONG = false: tiles of 1..512 pairs (R <= 8); LONG = true: 513..1024 pairs (R = 16, more VGPRs,
-// separate launch so the short-list kernel keeps its occupancy).  Longer lists: k_tile_sort.
-// `tiles` holds exactly the tiles of this path (built by k_bin_scan).
-template <bool LONG>
-__global__ __launch_bounds__(256) void k_tile_sort_wave(int count, const uint32_t *__restrict__ tiles,
-                                                        const uint2 *__restrict__ ranges,
-                                                        const uint64_t *__restrict__ keys,
-                                                        const uint32_t *__restrict__ vals,
-                                                        uint32_t *__restrict__ point_list,
-                                                        uint32_t *__restrict__ slot_emit) {
-    const int w = blockIdx.x * kTilesPerBlock + (threadIdx.x >> 6);
-    if (w >= count) return;
-    const int lane = threadIdx.x & 63;
-    const uint2 rg = ranges[tiles[w]];
-    const int n = (int)(rg.y - rg.x);
-    if (LONG) {
-        tile_sort_regs<16>(n, rg.x, keys, vals, point_list, slot_emit, lane);
-        return;
-    }
-    if (n <= 64) tile_sort_regs<1>(n, rg.x, keys, vals, point_list, slot_emit, lane);
-    else if (n <= 128) tile_sort_regs<2>(n, rg.x, keys, vals, point_list, slot_emit, lane);
-    else if (n <= 256) tile_sort_regs<4>(n, rg.x, keys, vals, point_list, slot_emit, lane);
-    else tile_sort_regs<8>(n, rg.x, keys, vals, point_list, slot_emit, lane);
+    for (int r = 0; r < R; ++r) { s_key[ibase + r] = k[r]; s_val[ibase + r] = v[r]; }
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
@@ -456,53 +458,85 @@ __global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint32_t *__res
 }
 
 // ------------------------------------------------------------------------------------------
-// Front-to-back blend.  One 256-thread block per 16x16 tile; wave w owns pixel rows 4w..4w+3 (one
-// pixel per lane) and walks the tile's list on its own: wave-private LDS staging, no block
-// barriers, early exit per 64 pixels.  Tiles are dispatched longest list first (tile_order).
-// Gaussians are staged one per lane in batches of 64 (one gather of the 64-byte render record) and
-// a conservative ellipse test against the wave's 16x4 pixel rectangle drops pairs that cannot reach
-// alpha >= 1/255 there; the per-pixel update is branch-free (selects + FMAs).
+// Per-tile depth sort + front-to-back blend.  One 256-thread block per 16x16 tile, dispatched
+// longest list first (tile_order).  A list of up to kFwdSortCap pairs is first depth-sorted by the
+// block (block_sort_tile: registers + three LDS exchange stages), which also writes the backward's
+// point_list / slot_emit; longer lists were sorted beforehand by k_tile_sort.  The blend walks the
+// sorted list in batches of 64: the block stages each batch once (thread 4e + q gathers entry e's
+// render record and tests it against quarter q = pixel rows 4q..4q+3 with a conservative ellipse
+// bound), then wave q blends its 16x4 quarter (one pixel per lane) over the entries whose bit q is
+// set; saturated quarters skip their evaluations and the walk ends when all four are saturated.
 __global__ __launch_bounds__(256) void k_render_fwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
-    const uint32_t *__restrict__ point_list, const float4 *__restrict__ rec, const float *__restrict__ bg,
-    float *__restrict__ out_color, float *__restrict__ out_depth, float *__restrict__ final_T,
-    uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc, uint32_t *__restrict__ tile_cost) {
-    __shared__ float4 s_rec[kTilesPerBlock][3][64];
-    const int wv = threadIdx.x >> 6;
-    float4(&s_a)[64] = s_rec[wv][0];
-    float4(&s_b)[64] = s_rec[wv][1];
-    float4(&s_c)[64] = s_rec[wv][2];
+    const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+    uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
+    const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
+    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
+    uint32_t *__restrict__ tile_cost) {
+    __shared__ uint64_t s_key[kFwdSortCap];
+    __shared__ union {
+        uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
+        struct {
+            float4 rec[3][64];      // then: the staged batch of 64 render records
+            uint32_t q[64];         // and their quarter masks
+        } st;
+    } s_u;
+    __shared__ uint32_t s_live;     // quarters (bits) with an unsaturated pixel
     const int tile = (int)tile_order[blockIdx.x];
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    const bool sorted_here = n <= kFwdSortCap;
+    if (n > 0 && sorted_here) {
+        if (n <= 256) block_sort_tile<1>(n, rg.x, keys, vals, s_key, s_u.val);
+        else if (n <= 512) block_sort_tile<2>(n, rg.x, keys, vals, s_key, s_u.val);
+        else block_sort_tile<4>(n, rg.x, keys, vals, s_key, s_u.val);
+        for (int i = threadIdx.x; i < n; i += 256) {
+            point_list[rg.x + i] = (uint32_t)s_key[i];
+            slot_emit[rg.x + i] = s_u.val[i];
+        }
+    }
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = tile % gx, ty = tile / gx;
-    const int lane = threadIdx.x & 63;
     const int px = tx * kTileW + (lane & 15);
     const int py = ty * kTileH + 4 * wv + (lane >> 4);
     const float pfx = (float)px, pfy = (float)py;
-    const float rx0 = (float)(tx * kTileW), ry0 = (float)(ty * kTileH + 4 * wv);
-    const float rx1 = rx0 + (kTileW - 1), ry1 = ry0 + 3;
-    const uint2 rg = ranges[tile];
-    const int n = (int)(rg.y - rg.x);
+    // staging role: thread 4e + q handles entry e of the batch against quarter q
+    const int se = threadIdx.x >> 2, sq = threadIdx.x & 3;
+    const float qx0 = (float)(tx * kTileW), qy0 = (float)(ty * kTileH + 4 * sq);
     const bool inside = px < W && py < H;
     bool done = !inside;
+    if (threadIdx.x == 0) s_live = 0;
+    __syncthreads();  // sort outputs consumed / s_live cleared
+    if (__ballot(!done) && lane == 0) atomicOr(&s_live, 1u << wv);
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
     uint32_t last = 0;
     for (int base = 0; base < n; base += 64) {
-        if (!__ballot(!done)) break;
-        const int idx = base + lane;
-        bool live = false;
+        __syncthreads();  // previous batch fully consumed; s_live up to date
+        const uint32_t live = s_live;
+        if (!live) break;
+        // ---- stage the batch (block-wide) ----
+        const int idx = base + se;
+        bool hit = false;
         if (idx < n) {
-            const uint32_t g = point_list[rg.x + idx];
-            const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
-            s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
-            live = !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, rx0, ry0, rx1, ry1);
+            const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
+            const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1];
+            if (sq < 3) s_u.st.rec[sq][se] = rec[(size_t)kRecF4 * g + sq];
+            hit = ((live >> sq) & 1u) &&
+                  !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kTileW - 1), qy0 + 3);
         }
-        uint64_t m = __ballot(live);
-        wave_lds_sync();
+        // combine the 4 quarter bits of entry se (lanes 4e..4e+3 of this wave) with DPP
+        uint32_t bits = hit ? (1u << sq) : 0u;
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xF, 0xF, false);  // xor 1
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xF, 0xF, false);  // xor 2
+        if (sq == 0) s_u.st.q[se] = bits;
+        __syncthreads();
+        // ---- blend this wave's quarter ----
+        uint64_t m = __ballot((s_u.st.q[lane] >> wv) & 1u);
+        if (!((live >> wv) & 1u)) m = 0;
         while (m) {
-            if (!__ballot(!done)) break;
             const int j = __builtin_ctzll(m);
             m &= m - 1;
-            const float4 a = s_a[j], b = s_b[j], c = s_c[j];
+            const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
             const Blend e = blend_eval(a, b, pfx, pfy);
             const bool ok = !done && blend_ok(e);
             const float test_T = Tt * (1.f - e.alpha);
@@ -517,7 +551,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             Tt = use ? test_T : Tt;
             last = use ? (uint32_t)(base + j + 1) : last;
         }
-        wave_lds_sync();
+        if (((live >> wv) & 1u) && !__ballot(!done) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
     if (inside) {
         const int pid = py * W + px;
@@ -609,25 +643,18 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(const FwdArgs &a, const uint32_t *n_per_path, hipStream_t s) {
-    const int T = a.gx * a.gy;
-    const uint32_t *lists = a.sort_lists;
-    if (n_per_path[0])
-        k_tile_sort_wave<false><<<div_up((int)n_per_path[0], kTilesPerBlock), 256, 0, s>>>(
-            (int)n_per_path[0], lists, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
-    if (n_per_path[1])
-        k_tile_sort_wave<true><<<div_up((int)n_per_path[1], kTilesPerBlock), 256, 0, s>>>(
-            (int)n_per_path[1], lists + T, a.ranges, a.keys, a.vals, a.point_list, a.slot_emit);
-    if (n_per_path[2])
-        k_tile_sort<<<n_per_path[2], 256, sizeof(uint64_t) * kSortCap, s>>>(
-            a.gx, lists + 2 * T, a.ranges, a.keys, a.rect, a.goff, a.point_list, a.slot_emit);
+hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_long, hipStream_t s) {
+    // lists of up to kFwdSortCap pairs are sorted inside k_render_fwd; only longer ones here
+    if (n_long == 0) return hipSuccess;
+    k_tile_sort<<<n_long, 256, sizeof(uint64_t) * kSortCap, s>>>(a.gx, a.sort_lists, a.ranges, a.keys,
+                                                                 a.rect, a.goff, a.point_list, a.slot_emit);
     return hipGetLastError();
 }
 
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
-    k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.point_list, a.rec,
-                                   a.bg, a.out_color, a.out_depth, a.final_T, a.n_contrib,
+    k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.keys, a.vals,
+                                   a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.final_T, a.n_contrib,
                                    a.tile_maxc, a.tile_cost);
     return hipGetLastError();
 }
