@@ -270,8 +270,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     if (g->P == 0) return GSR_OK;
     if (!geom || !binning || !image || !dL_dcolor || !radii || !alloc)
         return fail(GSR_ERR_ARG, "gsr_backward: missing saved buffers / dL_dcolor / allocator");
-    if (!out->dL_dmeans2D || !out->dL_dcolors || !out->dL_dopacity || !out->dL_dmeans3D ||
-        !out->dL_dcov3D || !out->dL_dscales || !out->dL_drotations || (g->shs && !out->dL_dsh))
+    if (!out->dL_dmeans2D || !out->dL_dopacity || !out->dL_dmeans3D || (g->shs && !out->dL_dsh))
         return fail(GSR_ERR_ARG, "gsr_backward: missing gradient output");
     if (num_rendered < 0) return fail(GSR_ERR_ARG, "num_rendered < 0");
     hipStream_t s = (hipStream_t)stream;

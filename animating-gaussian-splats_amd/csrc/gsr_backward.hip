@@ -108,14 +108,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         // quarter whose pixels all precede this slot in the forward's order (p >= its max
         // n_contrib) is skipped too
         uint32_t qmask = 0;
-        float4 cj = make_float4(0.f, 0.f, 0.f, 0.f);  // exact conic of the Gaussian this lane staged
-        uint32_t em = 0;                              // emission index of the pair this lane staged
+        uint32_t g_st = 0;  // Gaussian this lane staged (its record is re-read for the epilogue)
         if (lane < cnt) {
             const uint32_t p = (uint32_t)(start + lane);
             const uint32_t g = point_list[rg.x + p];
-            em = slot_emit[rg.x + p];
+            g_st = g;
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
-            cj = rec[(size_t)kRecF4 * g + 3];
             s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
             const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
 #pragma unroll
@@ -143,7 +141,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
                 if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
                 // branch-free: a non-contributing pixel gets alpha = 0, which makes every update an
                 // identity (r = 1, AR unchanged, zero sums)
-                const float dy = a.y - pfy[k];
+                const float dy = a.y - pfy[k];  // same operation as the forward's (bitwise-equal decisions)
                 const float p2 = pair_power(x, b.x, dy);
                 const float G = __builtin_amdgcn_exp2f(p2);
                 const float alpha = fminf(0.99f, b.y * G);
@@ -179,6 +177,8 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         }
         wave_lds_sync();
         if (lane < cnt) {
+            const float4 cj = rec[(size_t)kRecF4 * g_st + 3];  // exact conic (a, b, c)
+            const uint32_t em = slot_emit[rg.x + start + lane];
             const float *sm = s_out + lane * kPartial;
             const float S1 = sm[0], S2 = sm[1];
             float4 *dst = part + 3 * (size_t)em;
@@ -326,17 +326,23 @@ __device__ inline void gauss_bwd_one(
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec) {
+    // dL_dcolors / dL_dcov3D / dL_dscales / dL_drot may be NULL (gradient not requested)
     if (!(radii[i] > 0)) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            dL_dmeans2D[3 * i + k] = 0.f; dL_dcolors[3 * i + k] = 0.f; dL_dmeans3D[3 * i + k] = 0.f;
-            dL_dscales[3 * i + k] = 0.f;
+            dL_dmeans2D[3 * i + k] = 0.f; dL_dmeans3D[3 * i + k] = 0.f;
+            if (dL_dcolors) dL_dcolors[3 * i + k] = 0.f;
+            if (dL_dscales) dL_dscales[3 * i + k] = 0.f;
         }
         dL_dopacity[i] = 0.f;
+        if (dL_dcov3D) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = 0.f;
+            for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = 0.f;
+        }
+        if (dL_drot) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dL_drot[4 * i + k] = 0.f;
+            for (int k = 0; k < 4; ++k) dL_drot[4 * i + k] = 0.f;
+        }
         if (MC > 0) {
 #pragma unroll
             for (int k = 0; k < 3 * MC; ++k) s_row[k] = 0.f;
@@ -363,7 +369,7 @@ __device__ inline void gauss_bwd_one(
     } else {
         dL_dopacity[i] = acc[5];
     }
-    dL_dcolors[3 * i] = acc[6]; dL_dcolors[3 * i + 1] = acc[7]; dL_dcolors[3 * i + 2] = acc[8];
+    if (dL_dcolors) { dL_dcolors[3 * i] = acc[6]; dL_dcolors[3 * i + 1] = acc[7]; dL_dcolors[3 * i + 2] = acc[8]; }
     const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
 
     float vm[16], pj[16];
@@ -421,8 +427,10 @@ __device__ inline void gauss_bwd_one(
 #pragma unroll
         for (int k = 0; k < 6; ++k) dcov[k] = 0;
     }
+    if (dL_dcov3D) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = dcov[k];
+        for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = dcov[k];
+    }
 #define VV(cc, rr) GM(V, cc, rr)
     const float dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
                        (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_db;
@@ -482,11 +490,11 @@ __device__ inline void gauss_bwd_one(
         cov3d_backward(s3, scale_modifier, q, dcov, ds, dr);
         if (act & GSR_ACT_EXP_SCALES) { ds.x *= s3.x; ds.y *= s3.y; ds.z *= s3.z; }
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) dr = act_normalize_bwd(q, qn, dr);
-        dL_dscales[3 * i] = ds.x; dL_dscales[3 * i + 1] = ds.y; dL_dscales[3 * i + 2] = ds.z;
-        dL_drot[4 * i] = dr.x; dL_drot[4 * i + 1] = dr.y; dL_drot[4 * i + 2] = dr.z; dL_drot[4 * i + 3] = dr.w;
+        if (dL_dscales) { dL_dscales[3 * i] = ds.x; dL_dscales[3 * i + 1] = ds.y; dL_dscales[3 * i + 2] = ds.z; }
+        if (dL_drot) { dL_drot[4 * i] = dr.x; dL_drot[4 * i + 1] = dr.y; dL_drot[4 * i + 2] = dr.z; dL_drot[4 * i + 3] = dr.w; }
     } else {
-        dL_dscales[3 * i] = 0.f; dL_dscales[3 * i + 1] = 0.f; dL_dscales[3 * i + 2] = 0.f;
-        dL_drot[4 * i] = 0.f; dL_drot[4 * i + 1] = 0.f; dL_drot[4 * i + 2] = 0.f; dL_drot[4 * i + 3] = 0.f;
+        if (dL_dscales) { dL_dscales[3 * i] = 0.f; dL_dscales[3 * i + 1] = 0.f; dL_dscales[3 * i + 2] = 0.f; }
+        if (dL_drot) { dL_drot[4 * i] = 0.f; dL_drot[4 * i + 1] = 0.f; dL_drot[4 * i + 2] = 0.f; dL_drot[4 * i + 3] = 0.f; }
     }
 }
 

@@ -284,14 +284,21 @@ __device__ inline void tile_sort_write(uint64_t key, uint32_t slot, int tx, int 
 
 // ---- wave-level register bitonic sort (gfx950 cross-lane ops) ------------------------------
 // Element i = lane * R + r lives in register r of `lane`: exchanges at distance < R stay inside a
-// lane, larger distances are lane xors d = dist / R done with DPP (d = 1, 2), ds_swizzle
-// (d = 4, 8, 16) or v_permlane32_swap (d = 32).
+// lane, larger distances are lane xors d = dist / R, all on the VALU (no LDS round trip):
+// d = 1, 2 DPP quad_perm; d = 4 DPP row_half_mirror then quad reversal; d = 8 DPP row_ror:8;
+// d = 16, 32 v_permlane16_swap / v_permlane32_swap.
 template <int D>
 __device__ inline uint32_t lane_xor(uint32_t x) {
     if constexpr (D == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
     else if constexpr (D == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
-    else if constexpr (D == 4 || D == 8 || D == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (D << 10));
-    else {
+    else if constexpr (D == 4) {
+        const int m = __builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // i -> 7 - i per 8 lanes
+        return (uint32_t)__builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, false);     // reverse each quad
+    } else if constexpr (D == 8) return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);
+    else if constexpr (D == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (threadIdx.x & 16) ? r[0] : r[1];
+    } else {
         auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
         return (threadIdx.x & 32) ? r[0] : r[1];
     }
@@ -310,10 +317,10 @@ __device__ inline void bitonic_xlane(uint64_t (&k)[R], uint32_t (&v)[R], bool ta
     }
 }
 
-// Stages j = J, J/2, ..., 1 (J < 64 R) of the bitonic merge of size KK, on the wave's elements
-// i = gbase + lane * R + r (ascending where (i & KK) == 0).
-template <int R, int KK, int J>
-__device__ inline void wave_merge_stages(uint64_t (&k)[R], uint32_t (&v)[R], int lane, uint32_t gbase) {
+// Stages j = J, J/2, ..., 1 (J < 64 R) of the bitonic merge of size kk, on the wave's elements
+// i = gbase + lane * R + r (ascending where (i & kk) == 0).
+template <int R, int J>
+__device__ inline void wave_merge_stages(uint64_t (&k)[R], uint32_t (&v)[R], int lane, uint32_t gbase, uint32_t KK) {
     if constexpr (J > 0) {
         if constexpr (J < R) {
 #pragma unroll
@@ -332,7 +339,7 @@ __device__ inline void wave_merge_stages(uint64_t (&k)[R], uint32_t (&v)[R], int
             const bool take_min = ((lane & D) == 0) == asc;
             bitonic_xlane<R, D>(k, v, take_min);
         }
-        wave_merge_stages<R, KK, J / 2>(k, v, lane, gbase);
+        wave_merge_stages<R, J / 2>(k, v, lane, gbase, KK);
     }
 }
 
@@ -341,7 +348,7 @@ __device__ inline void wave_merge_stages(uint64_t (&k)[R], uint32_t (&v)[R], int
 template <int R, int KK>
 __device__ inline void wave_sort_stages(uint64_t (&k)[R], uint32_t (&v)[R], int lane, uint32_t gbase) {
     if constexpr (KK <= 64 * R) {
-        wave_merge_stages<R, KK, KK / 2>(k, v, lane, gbase);
+        wave_merge_stages<R, KK / 2>(k, v, lane, gbase, KK);
         wave_sort_stages<R, 2 * KK>(k, v, lane, gbase);
     }
 }
@@ -366,11 +373,12 @@ __device__ inline void block_xchg_stage(uint64_t (&k)[R], uint32_t (&v)[R], uint
     __syncthreads();
 }
 
-// Sort one tile's n <= 256 R (key, emission) pairs with the block's 4 waves: each wave sorts its
-// 64 R-element segment in registers (DPP / swizzle / permlane exchanges), then the two cross-wave
-// merge levels exchange through LDS and finish in registers.  Leaves the sorted keys in s_key[0, n)
-// and emissions in s_val[0, n).  Keys are (depth_bits << 32 | index), unique inside a tile.
-template <int R>
+// Sort one tile's n <= 64 R NW (key, emission) pairs with the block's NW waves: each wave sorts its
+// 64 R-element segment in registers (DPP / swizzle / permlane exchanges), then every cross-wave
+// merge level exchanges through LDS for distances >= 64 R and finishes in registers.  Leaves the
+// sorted keys in s_key[0, n) and emissions in s_val[0, n).  Keys are (depth_bits << 32 | index),
+// unique inside a tile.
+template <int R, int NW>
 __device__ inline void block_sort_tile(int n, uint32_t start, const uint64_t *__restrict__ keys,
                                        const uint32_t *__restrict__ vals, uint64_t *s_key, uint32_t *s_val) {
     constexpr int SEG = 64 * R;
@@ -385,47 +393,41 @@ __device__ inline void block_sort_tile(int n, uint32_t start, const uint64_t *__
         v[r] = i < n ? vals[start + i] : 0u;
     }
     wave_sort_stages<R, 2>(k, v, lane, gbase);
-    // merge of size 2 SEG: one LDS stage (j = SEG), then j < SEG in registers
-    block_xchg_stage<R>(k, v, ibase, 2 * SEG, SEG, s_key, s_val);
-    wave_merge_stages<R, 2 * SEG, SEG / 2>(k, v, lane, gbase);
-    // merge of size 4 SEG (the whole block): j = 2 SEG and SEG through LDS, then registers
-    block_xchg_stage<R>(k, v, ibase, 4 * SEG, 2 * SEG, s_key, s_val);
-    block_xchg_stage<R>(k, v, ibase, 4 * SEG, SEG, s_key, s_val);
-    wave_merge_stages<R, 4 * SEG, SEG / 2>(k, v, lane, gbase);
+    for (uint32_t kk = 2 * SEG; kk <= (uint32_t)(NW * SEG); kk <<= 1) {
+        for (uint32_t j = kk >> 1; j >= (uint32_t)SEG; j >>= 1) block_xchg_stage<R>(k, v, ibase, kk, j, s_key, s_val);
+        wave_merge_stages<R, SEG / 2>(k, v, lane, gbase, kk);
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) { s_key[ibase + r] = k[r]; s_val[ibase + r] = v[r]; }
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
-                                                   const uint2 *__restrict__ ranges,
-                                                   uint64_t *__restrict__ keys,
-                                                   const uint2 *__restrict__ rects,
-                                                   const uint32_t *__restrict__ goff,
-                                                   uint32_t *__restrict__ point_list,
-                                                   uint32_t *__restrict__ slot_emit) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_keys[];
+// Tiles longer than kFwdSortCap (one 512-thread block each, launched only for those tiles): up to
+// kSortCap pairs with the register + LDS hybrid of block_sort_tile over 8 waves (4 or 8 keys per
+// lane); beyond that an in-place bitonic network in global memory.
+__global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
+                                                    const uint2 *__restrict__ ranges,
+                                                    uint64_t *__restrict__ keys,
+                                                    const uint32_t *__restrict__ vals,
+                                                    const uint2 *__restrict__ rects,
+                                                    const uint32_t *__restrict__ goff,
+                                                    uint32_t *__restrict__ point_list,
+                                                    uint32_t *__restrict__ slot_emit) {
+    __shared__ uint64_t s_keys[kSortCap];
+    __shared__ uint32_t s_vals[kSortCap];
     const int tile = (int)tiles[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
     const int tx = tile % gx, ty = tile / gx;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (n <= kSortCap) {
-        int np = 1;
-        while (np < n) np <<= 1;
-        for (int i = tid; i < np; i += nt) s_keys[i] = i < n ? keys[rg.x + i] : ~0ull;
-        __syncthreads();
-        for (int k = 2; k <= np; k <<= 1)
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = tid; i < (np >> 1); i += nt) {
-                    const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
-                    const bool asc = (lo & k) == 0;
-                    const uint64_t a = s_keys[lo], c = s_keys[hi];
-                    if ((a > c) == asc) { s_keys[lo] = c; s_keys[hi] = a; }
-                }
-                __syncthreads();
-            }
-        for (int i = tid; i < n; i += nt) tile_sort_write(s_keys[i], rg.x + i, tx, ty, rects, goff, point_list, slot_emit);
+        static_assert(kSortCap == 8 * 64 * 8, "k_tile_sort: 8 waves x 64 lanes x 8 keys");
+        if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, keys, vals, s_keys, s_vals);
+        else block_sort_tile<8, 8>(n, rg.x, keys, vals, s_keys, s_vals);
+        for (int i = tid; i < n; i += nt) {
+            point_list[rg.x + i] = (uint32_t)s_keys[i];
+            slot_emit[rg.x + i] = s_vals[i];
+        }
     } else {
         // long tile: in-place bitonic network in global memory with virtual +inf padding
         // ("flip" form: every comparator puts the minimum at the lower index).
@@ -487,9 +489,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const int n = (int)(rg.y - rg.x);
     const bool sorted_here = n <= kFwdSortCap;
     if (n > 0 && sorted_here) {
-        if (n <= 256) block_sort_tile<1>(n, rg.x, keys, vals, s_key, s_u.val);
-        else if (n <= 512) block_sort_tile<2>(n, rg.x, keys, vals, s_key, s_u.val);
-        else block_sort_tile<4>(n, rg.x, keys, vals, s_key, s_u.val);
+        if (n <= 256) block_sort_tile<1, 4>(n, rg.x, keys, vals, s_key, s_u.val);
+        else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, keys, vals, s_key, s_u.val);
+        else block_sort_tile<4, 4>(n, rg.x, keys, vals, s_key, s_u.val);
         for (int i = threadIdx.x; i < n; i += 256) {
             point_list[rg.x + i] = (uint32_t)s_key[i];
             slot_emit[rg.x + i] = s_u.val[i];
@@ -646,8 +648,8 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
 hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_long, hipStream_t s) {
     // lists of up to kFwdSortCap pairs are sorted inside k_render_fwd; only longer ones here
     if (n_long == 0) return hipSuccess;
-    k_tile_sort<<<n_long, 256, sizeof(uint64_t) * kSortCap, s>>>(a.gx, a.sort_lists, a.ranges, a.keys,
-                                                                 a.rect, a.goff, a.point_list, a.slot_emit);
+    k_tile_sort<<<n_long, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.keys, a.vals, a.rect, a.goff,
+                                        a.point_list, a.slot_emit);
     return hipGetLastError();
 }
 

@@ -204,7 +204,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
-                                 activations=0):
+                                 activations=0, skip_unused=False):
+    """Returns the 8 gradients of the upstream binding.  ``skip_unused``: gradients of inputs that
+    were not given (colours under SH, cov3D under scales/rotations and vice versa) come back as
+    empty tensors and their HBM writes are skipped."""
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
@@ -213,7 +216,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device
     e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731 - every element is written
-    out = (e(P, 3), e(P, 3), e(P, 1), e(P, 3), e(P, 6), e(P, M, 3), e(P, 3), e(P, 4))
+    has = lambda t: t is not None and t.numel() > 0  # noqa: E731
+    keep_col = not skip_unused or has(colors)
+    keep_cov = not skip_unused or has(cov3D_precomp)
+    keep_sr = not skip_unused or (has(scales) and has(rotations))
+    out = (e(P, 3), e(P, 3) if keep_col else e(0), e(P, 1), e(P, 3), e(P, 6) if keep_cov else e(0),
+           e(P, M, 3), e(P, 3) if keep_sr else e(0), e(P, 4) if keep_sr else e(0))
     if P == 0:
         return out
     dpix = dL_dout_color.contiguous().float()

@@ -73,7 +73,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                 sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp,
-         grad_sh, grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(*args)
+         grad_sh, grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(*args, skip_unused=True)
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities,
                 grad_scales, grad_rotations, grad_cov3Ds_precomp, None)
 
@@ -167,7 +167,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                 rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
                 rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                activations=_C.ACT_ALL)
+                activations=_C.ACT_ALL, skip_unused=True)
         need = ctx.needs_input_grad
         return (g_means, g_means2D if need[1] else None, g_sh if sh.numel() else None,
                 g_colors if colors.numel() else None, g_opacity.view(ctx.opacity_shape), g_scales, g_rot,

@@ -96,7 +96,10 @@ typedef struct gsr_gaussians {
 } gsr_gaussians;
 
 /* Gradient outputs of gsr_backward, in the order _C.rasterize_gaussians_backward returns them.
- * Every element of every non-NULL array is written (no pre-zeroing needed). */
+ * Every element of every non-NULL array is written (no pre-zeroing needed).  dL_dmeans2D,
+ * dL_dopacity, dL_dmeans3D (and dL_dsh when shs are given) are required; dL_dcolors, dL_dcov3D,
+ * dL_dscales and dL_drotations may be NULL when the caller does not need them (e.g. dL_dcolors
+ * under SH colour, dL_dcov3D when scales/rotations are given): their HBM writes are skipped. */
 typedef struct gsr_grads {
     float *dL_dmeans2D;   /* (P,3)  NDC units, z = 0 */
     float *dL_dcolors;    /* (P,3) */
