@@ -15,6 +15,10 @@
 
 namespace gsr {
 
+#ifdef GSR_TRACE
+__device__ uint64_t *g_trace_bwd;
+#endif
+
 // Backward dispatch order (one block): tiles by descending sum of n_contrib over their pixels.
 __global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *__restrict__ tile_cost,
                                                          uint32_t *__restrict__ tile_order) {
@@ -47,6 +51,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const int wv = threadIdx.x >> 6;
     const int t_lin = blockIdx.x * kTilesPerBlock + wv;
     if (t_lin >= T) return;
+#ifdef GSR_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     float4(&s_a)[64] = s_rec[wv][0];
     float4(&s_b)[64] = s_rec[wv][1];
     float4(&s_c)[64] = s_rec[wv][2];
@@ -78,7 +85,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     // needs the projection of accum_rec on dL/dpixel, and folding eagerly right after each
     // contributor (AR <- AR + alpha (<c, dL/dpix> - AR)) gives the same value with the same
     // rounding, while a non-contributing pair (alpha = 0) leaves it untouched without a select.
-    float Tt[4], tbg[4], dp0[4], dp1[4], dp2[4], AR[4], pfy[4];
+    // The reference's background term -T_final / (1 - alpha) <bg, dL/dpix> is carried inside AR:
+    // starting the recurrence at AR = <bg, dL/dpix> (the background seen through T_final) gives
+    // exactly T_before * (<c, dL/dpix> - AR) = reference dL/dalpha, with no per-pair bg term.
+    float Tt[4], dp0[4], dp1[4], dp2[4], AR[4], pfy[4];
     uint32_t lastc[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -94,8 +104,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         dp2[k] = inside ? dL_dpixels[2 * H * W + pid] : 0.f;
         float bd = 0;
         bd += bg0 * dp0[k]; bd += bg1 * dp1[k]; bd += bg2 * dp2[k];
-        tbg[k] = -Tf * bd;  // background term of dL/dalpha: -T_final / (1 - alpha) * <bg, dL/dpix>
-        AR[k] = 0.f;
+        AR[k] = bd;
     }
     const int row = lane >> 4;
     const int slot0123 = (row == 0) ? 0 : (row == 1) ? 2 : (row == 2) ? 1 : 3;  // wave_sum9 lane map
@@ -152,7 +161,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
                 Tt[k] = Tt[k] * r;
                 const float cd = fmaf(c.z, dp2[k], fmaf(c.y, dp1[k], c.x * dp0[k]));  // <colour, dL/dpix>
                 const float diff = cd - AR[k];
-                const float dLa = fmaf(r, tbg[k], diff * Tt[k]);
+                const float dLa = diff * Tt[k];
                 AR[k] = fmaf(al, diff, AR[k]);
                 const float gd = ok ? G * dLa : 0.f;
                 const float u = gd * dy;
@@ -190,6 +199,9 @@ __global__ __launch_bounds__(256) void k_render_bwd(
             dst[2] = make_float4(sm[8], 0.f, 0.f, 0.f);                // dcolour.b
         }
     }
+#ifdef GSR_TRACE
+    trace_wave(g_trace_bwd, t_lin, t_start);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -573,3 +585,9 @@ hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {
 }
 
 }  // namespace gsr
+
+#ifdef GSR_TRACE
+extern "C" int gsr_debug_trace_bwd(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_trace_bwd), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
+}
+#endif

@@ -52,10 +52,11 @@ struct GeomLayout {
 };
 
 // Binning work decomposition over Gaussians: NB chunks of CH Gaussians (CH multiple of 256).
+constexpr int kBinThreads = 1024;  // threads per binning block (one chunk of CH Gaussians)
 struct BinGrid {
     int CH, NB;
     __host__ __device__ BinGrid(int P) {
-        int c = div_up(P, 256);
+        int c = div_up(P, 512);  // ~512 chunks (2 per CU)
         c = div_up(c, 256) * 256;
         CH = c < 1024 ? 1024 : c;
         NB = P > 0 ? div_up(P, CH) : 0;
@@ -314,6 +315,19 @@ __device__ inline float wave_sum_lane63(float v) {
 
 constexpr int kTilesPerBlock = 4;
 #define GSR_LOG2E 1.4426950408889634f
+
+// Diagnostic builds (make trace -> libgsr_trace.so): every render wave stores (start, end,
+// HW_ID) with s_memrealtime (100 MHz, chip-wide) into a buffer registered by
+// gsr_debug_trace_{fwd,bwd}; compiled out of libgsr.so.
+#ifdef GSR_TRACE
+__device__ inline void trace_wave(uint64_t *buf, int slot, uint64_t t0) {
+    if (buf && (threadIdx.x & 63) == 0) {
+        buf[3 * slot] = t0;
+        buf[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+        buf[3 * slot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+    }
+}
+#endif
 
 // Blend weight of one (pixel, Gaussian) pair, shared by the forward and backward kernels so that
 // both take identical decisions: power2 = power * log2(e) evaluated with FMAs, G = 2^power2.

@@ -20,6 +20,10 @@
 
 namespace gsr {
 
+#ifdef GSR_TRACE
+__device__ uint64_t *g_trace_fwd;
+#endif
+
 // ------------------------------------------------------------------------------------------
 template <int MC>  // SH coefficient count staged through LDS (0: direct loads / no SH)
 __global__ __launch_bounds__(256) void k_preprocess(
@@ -108,7 +112,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
 // Tile histogram per chunk of Gaussians.  USE_LDS: histogram in LDS (T <= kMaxLdsTiles), then one
 // global atomic per non-empty (chunk, tile) bin -- lanes of a wave add to 64 consecutive counters.
 template <bool USE_LDS>
-__global__ __launch_bounds__(256) void k_bin_count(int P, int CH, int T, int gx,
+__global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T, int gx,
                                                    const uint2 *__restrict__ rects,
                                                    const uint32_t *__restrict__ tiles,
                                                    uint32_t *__restrict__ tile_count,
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
 // contiguous slab per non-empty tile with a single global atomic, then hands out slots from LDS.
 // The order inside a tile is arbitrary here; k_tile_sort makes it canonical.
 template <bool USE_LDS>
-__global__ __launch_bounds__(256) void k_bin_emit(int P, int CH, int T, int gx,
+__global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, int gx,
                                                   const uint2 *__restrict__ rects,
                                                   const uint32_t *__restrict__ tiles,
                                                   const float *__restrict__ depth,
@@ -484,6 +488,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         } st;
     } s_u;
     __shared__ uint32_t s_live;     // quarters (bits) with an unsaturated pixel
+#ifdef GSR_TRACE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const int tile = (int)tile_order[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -571,6 +578,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         sum += (uint32_t)__shfl_xor((int)sum, d, 64);
     }
     if (lane == 0) { tile_maxc[4 * tile + wv] = mx; tile_cost[4 * tile + wv] = sum; }
+#ifdef GSR_TRACE
+    trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
+#endif
 }
 
 __global__ void k_zero_f32(float *p, size_t n) {
@@ -620,9 +630,9 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     if (e != hipSuccess) return e;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_count<true><<<bg.NB, 256, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
+        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
     else
-        k_bin_count<false><<<bg.NB, 256, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
+        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
     return hipGetLastError();
 }
 
@@ -639,9 +649,9 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_emit<true><<<bg.NB, 256, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
+        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
     else
-        k_bin_emit<false><<<bg.NB, 256, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
+        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
     return hipGetLastError();
 }
 
@@ -675,3 +685,9 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 }
 
 }  // namespace gsr
+
+#ifdef GSR_TRACE
+extern "C" int gsr_debug_trace_fwd(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_trace_fwd), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
+}
+#endif
