@@ -8,6 +8,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <chrono>
 #include <map>
@@ -312,6 +313,78 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
     if (P < 0) return fail(GSR_ERR_ARG, "P must be >= 0");
     if (P > 0 && (!means3D || !viewmatrix || !present)) return fail(GSR_ERR_ARG, "null pointer");
     HIP_TRY(launch_mark_visible(P, means3D, viewmatrix, present, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+}  // extern "C"
+
+// ---- fused L1 + SSIM ----------------------------------------------------------------------
+namespace {
+struct SsimScratch {
+    size_t maps, partial, total;
+    SsimScratch(int planes, int H, int W) {
+        const size_t n = (size_t)planes * H * W;
+        maps = 0;
+        partial = align256(sizeof(float) * 3 * n);
+        total = align256(partial + sizeof(float2) * ssim_partials(planes, H, W));
+    }
+};
+
+// The window of calc_ssim: gaussian(11, 1.5) (external.py:48-55) evaluates exp() in double, stores
+// float32 and normalises by the float32 sum.
+SsimWindow ssim_window() {
+    SsimWindow w;
+    float sum = 0.f;
+    for (int x = 0; x < 11; ++x) {
+        w.w[x] = (float)std::exp(-(double)((x - 5) * (x - 5)) / (2.0 * 1.5 * 1.5));
+        sum += w.w[x];
+    }
+    for (int x = 0; x < 11; ++x) w.w[x] = w.w[x] / sum;
+    return w;
+}
+
+int check_ssim(int planes, int H, int W, const float *img1, const float *img2) {
+    if (planes < 0 || H < 0 || W < 0) return fail(GSR_ERR_ARG, "l1_ssim: negative size");
+    if ((size_t)planes * H * W > 0 && (!img1 || !img2)) return fail(GSR_ERR_ARG, "l1_ssim: null image");
+    if ((size_t)planes * H * W >= (size_t)1 << 31) return fail(GSR_ERR_UNSUPPORTED, "l1_ssim: image too large");
+    if (planes > 65535) return fail(GSR_ERR_UNSUPPORTED, "l1_ssim: more than 65535 planes");
+    return GSR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+size_t gsr_ssim_scratch_bytes(int planes, int H, int W) {
+    return SsimScratch(planes < 0 ? 0 : planes, H < 0 ? 0 : H, W < 0 ? 0 : W).total;
+}
+
+int gsr_l1_ssim_forward(int planes, int H, int W, const float *img1, const float *img2, void *scratch,
+                        float *out_l1, float *out_ssim, void *stream) {
+    int rc = check_ssim(planes, H, W, img1, img2);
+    if (rc) return rc;
+    if (!out_l1 || !out_ssim) return fail(GSR_ERR_ARG, "l1_ssim: null output");
+    if ((size_t)planes * H * W == 0) return fail(GSR_ERR_ARG, "l1_ssim: empty image (the mean is undefined)");
+    if (!scratch) return fail(GSR_ERR_ARG, "l1_ssim: null scratch");
+    hipStream_t s = (hipStream_t)stream;
+    const SsimScratch L(planes, H, W);
+    char *base = (char *)scratch;
+    Phase ph(s, "ssim_fwd");
+    HIP_TRY(launch_ssim_fwd(planes, H, W, img1, img2, ssim_window(), (float *)(base + L.maps),
+                            (float2 *)(base + L.partial), out_l1, out_ssim, s));
+    return GSR_OK;
+}
+
+int gsr_l1_ssim_backward(int planes, int H, int W, const float *img1, const float *img2, const void *scratch,
+                         const float *dL_dl1, const float *dL_dssim, float *dL_dimg1, void *stream) {
+    int rc = check_ssim(planes, H, W, img1, img2);
+    if (rc) return rc;
+    if ((size_t)planes * H * W == 0) return GSR_OK;
+    if (!dL_dimg1 || !scratch) return fail(GSR_ERR_ARG, "l1_ssim: null gradient output / scratch");
+    hipStream_t s = (hipStream_t)stream;
+    const SsimScratch L(planes, H, W);
+    Phase ph(s, "ssim_bwd");
+    HIP_TRY(launch_ssim_bwd(planes, H, W, img1, img2, ssim_window(), (const float *)((const char *)scratch + L.maps),
+                            dL_dl1, dL_dssim, dL_dimg1, s));
     return GSR_OK;
 }
 

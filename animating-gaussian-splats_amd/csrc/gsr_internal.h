@@ -60,4 +60,13 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 
+// fused L1 + SSIM (gsr_loss.hip): normalised 1-D window of calc_ssim (external.py:48-65)
+struct SsimWindow { float w[11]; };
+size_t ssim_partials(int planes, int H, int W);
+hipError_t launch_ssim_fwd(int planes, int H, int W, const float *img1, const float *img2, const SsimWindow &w,
+                           float *maps, float2 *partial, float *out_l1, float *out_ssim, hipStream_t s);
+hipError_t launch_ssim_bwd(int planes, int H, int W, const float *img1, const float *img2, const SsimWindow &w,
+                           const float *maps, const float *g_l1, const float *g_ssim, float *dimg1,
+                           hipStream_t s);
+
 }  // namespace gsr

@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_bytes", "gsr_image_bytes",
     "gsr_binning_bytes", "gsr_scratch_bytes", "gsr_last_error", "gsr_abi_version",
     "gsr_profile_enable", "gsr_profile_select", "gsr_profile_reset", "gsr_profile_read", "gsr_buffer_offsets",
+    "gsr_ssim_scratch_bytes", "gsr_l1_ssim_forward", "gsr_l1_ssim_backward",
 )
 
 
@@ -95,13 +96,19 @@ def load_library():
     L.gsr_profile_read.restype = i
     L.gsr_buffer_offsets.restype = i
     L.gsr_buffer_offsets.argtypes = [i, i, i, i, ctypes.POINTER(ctypes.c_size_t), i]
+    L.gsr_ssim_scratch_bytes.restype = ctypes.c_size_t
+    L.gsr_ssim_scratch_bytes.argtypes = [i, i, i]
+    L.gsr_l1_ssim_forward.restype = i
+    L.gsr_l1_ssim_forward.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp]
+    L.gsr_l1_ssim_backward.restype = i
+    L.gsr_l1_ssim_backward.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, vp]
     if L.gsr_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libgsr.so ABI {L.gsr_abi_version()} != binding ABI {ABI_VERSION}: rebuild it")
     _lib = L
     return L
 
 
-ABI_VERSION = 2  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 3  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 

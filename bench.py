@@ -79,6 +79,62 @@ def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu):
                       f"oracle (oracle/gsr_oracle.c), {dt:.1f} s"}
 
 
+def _torch_calc_ssim(img1, img2):
+    """external.py:48-110 composed from torch ops (the reference's way: 5 grouped conv2d + elementwise),
+    for the loss leg's comparison only."""
+    from math import exp
+    g = torch.tensor([exp(-((x - 5) ** 2) / float(2 * 1.5 ** 2)) for x in range(11)])
+    g = (g / g.sum()).unsqueeze(1)
+    C = img1.size(-3)
+    w = g.mm(g.t()).float()[None, None].expand(C, 1, 11, 11).contiguous().to(img1.device)
+    conv = lambda t: torch.nn.functional.conv2d(t, w, padding=5, groups=C)  # noqa: E731
+    mu1, mu2 = conv(img1), conv(img2)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    s1, s2, s12 = conv(img1 * img1) - mu1_sq, conv(img2 * img2) - mu2_sq, conv(img1 * img2) - mu1_mu2
+    c1, c2 = 0.01 ** 2, 0.03 ** 2
+    return (((2 * mu1_mu2 + c1) * (2 * s12 + c2)) / ((mu1_sq + mu2_sq + c1) * (s1 + s2 + c2))).mean()
+
+
+def loss_call_site(steps, cam, leaves, dev):
+    """ms per render-loss fwd+bwd at the bench resolution (train.py:362-363): fused L1+SSIM kernels
+    (splat_loss) vs the reference's torch composition; plus the fused kernels' device times."""
+    import splat_loss
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    with torch.no_grad():
+        img = GaussianRasterizer(raster_settings=cam)(**leaves)[0].detach()
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    target = torch.rand(img.shape, generator=gen).to(dev)
+
+    def run(fn):
+        for _ in range(3):
+            x = img.clone().requires_grad_(True)
+            fn(x).backward()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            x = img.clone().requires_grad_(True)
+            fn(x).backward()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / steps * 1e3
+
+    fused = run(lambda x: splat_loss.image_loss(x, target))
+    ref = run(lambda x: 0.8 * torch.nn.functional.l1_loss(x, target) + 0.2 * (1.0 - _torch_calc_ssim(x, target)))
+    _C.profile_reset()
+    _C.profile_select(["ssim_fwd", "ssim_bwd"])
+    _C.profile_enable(True)
+    run(lambda x: splat_loss.image_loss(x, target))
+    _C.profile_enable(False)
+    k = {ph: _C.profile_read(ph) for ph in ("ssim_fwd", "ssim_bwd")}
+    _C.profile_select(None)
+    n = img.numel()
+    kms = {ph: v[0] / max(v[1], 1) for ph, v in k.items()}
+    return {"image": list(img.shape), "fused_ms": round(fused, 4), "torch_reference_ms": round(ref, 4),
+            "ssim_fwd_kernel_ms": round(kms["ssim_fwd"], 4), "ssim_bwd_kernel_ms": round(kms["ssim_bwd"], 4),
+            # algorithmic bytes: fwd 2 reads + 3 writes, bwd 5 reads + 1 write per pixel (fp32)
+            "ssim_fwd_GBps": round(20 * n / (kms["ssim_fwd"] * 1e-3) / 1e9, 1),
+            "ssim_bwd_GBps": round(24 * n / (kms["ssim_bwd"] * 1e-3) / 1e9, 1), "steps": steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +145,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--call-site-steps", type=int, default=10,
                     help="steps timed for each train.py call-site variant (0 = skip)")
+    ap.add_argument("--loss-steps", type=int, default=10,
+                    help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="untimed steps with events on every phase (per-kernel breakdown)")
     args = ap.parse_args()
@@ -216,6 +274,7 @@ def main():
                      "fused_activations_ms_per_view": round(fused_ms / per_view, 4),
                      "steps": args.call_site_steps}
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
+    loss_site = loss_call_site(args.loss_steps, cams[0], leaves, dev) if args.loss_steps > 0 else None
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
     import splat_dp
     used = sorted({ci for it in range(args.warmup + args.probe_steps, args.warmup + args.probe_steps + args.steps)
@@ -277,6 +336,7 @@ def main():
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
             "call_site": call_site,
+            "loss_call_site": loss_site,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

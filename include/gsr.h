@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 2
+#define GSR_ABI_VERSION 3
 
 enum gsr_status {
     GSR_OK = 0,
@@ -145,9 +145,28 @@ int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *o
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
 
+/* ---- Fused L1 + SSIM image loss (ABI >= 3) ------------------------------
+ * Replaces the loss of every render call site, train.py:362-363 / densify.py:127-129,149-151:
+ *     torch.nn.functional.l1_loss(img1, img2)  and  calc_ssim(img1, img2)   (external.py:68-110:
+ *     window_size 11, Gaussian sigma 1.5, zero padding 5, size_average=True)
+ * with one forward and one backward kernel pair.  img1/img2/dL_dimg1: `planes` contiguous fp32
+ * planes of height x width (a (3,H,W) image is 3 planes, a (B,C,H,W) batch B*C planes).  The
+ * scratch buffer (gsr_ssim_scratch_bytes) carries the per-pixel SSIM derivatives from the forward to
+ * the backward and must be kept alive between them. */
+size_t gsr_ssim_scratch_bytes(int planes, int height, int width);
+/* out_l1 = mean |img1 - img2|, out_ssim = mean SSIM: device float scalars (the values l1_loss and
+ * calc_ssim return). */
+int gsr_l1_ssim_forward(int planes, int height, int width, const float *img1, const float *img2,
+                        void *scratch, float *out_l1, float *out_ssim, void *stream);
+/* dL_dimg1 = dL_dl1 * d(l1)/d(img1) + dL_dssim * d(ssim)/d(img1); dL_dl1 / dL_dssim are DEVICE
+ * scalars (either may be NULL = 0), so no host synchronisation is needed.  img2 gets no gradient. */
+int gsr_l1_ssim_backward(int planes, int height, int width, const float *img1, const float *img2,
+                         const void *scratch, const float *dL_dl1, const float *dL_dssim,
+                         float *dL_dimg1, void *stream);
+
 /* Per-phase device timing with HIP events recorded on the call's stream (off by default).
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
- * "render_bwd", "gauss_bwd".  gsr_profile_read synchronises on the recorded events. */
+ * "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd".  gsr_profile_read synchronises on the recorded events. */
 int gsr_profile_enable(int on);
 /* Restrict event recording to a comma-separated list of phases (NULL or "" = every phase), so a
  * timed region can carry the events of one kernel only.  Host-side timers are unaffected. */

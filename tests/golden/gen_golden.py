@@ -9,7 +9,9 @@ What is captured:
     of train.py:460-503 (create_extrinsic_matrices / render_and_export_frame intrinsics)
   * create_render_arguments (shared.py:29-42) activations on a seeded parameter dict
   * build_rotation (external.py:27-46) - the quaternion convention of Sigma3D
-  * calc_ssim (external.py:68-110) on seeded images (for the fused-loss row of SURVEY 8(f))
+  * calc_ssim (external.py:68-110) on seeded images, with its autograd gradient, and the
+    0.8 * l1 + 0.2 * (1 - ssim) loss of densify.py:149-151 on a ragged binary-target pair (for the
+    fused-loss row of SURVEY 8(f))
   * update_max_2d_radii_and_visibility_mask (densify.py:154-162) + accumulate_mean_2d_gradients
     (external.py:113-124) over a sequence of seeded views, and densify_gaussians
     (external.py:211-314) at i = 500 with a seeded torch.normal - the statistics the data-parallel
@@ -106,6 +108,21 @@ def main():
     img2 = (img1 + 0.1 * torch.randn(3, 48, 64, generator=g)).clamp(0, 1)
     out["ssim_in_img1"], out["ssim_in_img2"] = img1.numpy(), img2.numpy()
     out["ssim_out"] = np.array(float(external.calc_ssim(img1, img2)))
+    x = img1.clone().requires_grad_(True)
+    external.calc_ssim(x, img2).backward()
+    out["ssim_out_grad"] = x.grad.numpy()
+    # the loss of densify.py:149-151 on a ragged segmentation-style pair (binary target), with the
+    # reference's autograd through calc_ssim and torch's l1_loss
+    seg = (torch.rand(3, 37, 53, generator=g) > 0.5).float()
+    rend = torch.sigmoid(3.0 * torch.randn(3, 37, 53, generator=g))
+    x = rend.clone().requires_grad_(True)
+    l1 = torch.nn.functional.l1_loss(x, seg)
+    ss = external.calc_ssim(x, seg)
+    loss = 0.8 * l1 + 0.2 * (1.0 - ss)
+    loss.backward()
+    out["loss_in_img1"], out["loss_in_img2"] = rend.numpy(), seg.numpy()
+    out["loss_out_l1"], out["loss_out_ssim"] = np.array(float(l1)), np.array(float(ss))
+    out["loss_out_grad"] = x.grad.numpy()
 
     # ---- densification statistics over a sequence of views ----------------------------------
     P = 2000
