@@ -388,6 +388,107 @@ int gsr_l1_ssim_backward(int planes, int H, int W, const float *img1, const floa
     return GSR_OK;
 }
 
+// ---- densification --------------------------------------------------------------------------
+}  // extern "C"
+namespace {
+int dens_args(const gsr_densify_settings *st, DensArgs &a) {
+    if (!st) return fail(GSR_ERR_ARG, "densify: null settings");
+    if (st->P < 0) return fail(GSR_ERR_ARG, "densify: P must be >= 0");
+    if (st->P > 0 && (!st->grad_accum || !st->vis_count || !st->log_scales || !st->opacity_logits ||
+                      !st->rotation_quaternions))
+        return fail(GSR_ERR_ARG, "densify: statistics / log_scales / opacity_logits / rotations required");
+    if (!(st->split_divisor > 0.f)) return fail(GSR_ERR_ARG, "densify: split_divisor must be > 0");
+    a.P = st->P; a.prune_big = st->prune_big;
+    a.grad_threshold = st->grad_threshold; a.small_scale = st->small_scale; a.big_scale = st->big_scale;
+    a.remove_opacity = st->remove_opacity;
+    // torch evaluates tensor / python-scalar on the GPU as tensor * (1 / scalar) in float
+    a.inv_split_div = 1.0f / st->split_divisor;
+    a.grad_accum = st->grad_accum; a.vis_count = st->vis_count; a.log_scales = st->log_scales;
+    a.opacity_logits = st->opacity_logits; a.rotations = st->rotation_quaternions;
+    return GSR_OK;
+}
+}  // namespace
+extern "C" {
+
+int gsr_densify_update_radii(int P, const int *radii, float *max_radii, uint8_t *visible, void *stream) {
+    if (P < 0) return fail(GSR_ERR_ARG, "densify: P must be >= 0");
+    if (P > 0 && (!radii || !max_radii || !visible)) return fail(GSR_ERR_ARG, "densify: null pointer");
+    HIP_TRY(launch_dens_radii(P, radii, max_radii, visible, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+int gsr_densify_accumulate_grads(int P, const uint8_t *visible, const float *means2D_grad, float *grad_accum,
+                                 float *vis_count, void *stream) {
+    if (P < 0) return fail(GSR_ERR_ARG, "densify: P must be >= 0");
+    if (P > 0 && (!visible || !means2D_grad || !grad_accum || !vis_count))
+        return fail(GSR_ERR_ARG, "densify: null pointer");
+    HIP_TRY(launch_dens_grads(P, visible, means2D_grad, grad_accum, vis_count, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+size_t gsr_densify_workspace_bytes(int P) { return DensWorkspace(P < 0 ? 0 : P).total; }
+
+int gsr_densify_plan(const gsr_densify_settings *st, void *workspace, gsr_densify_counts *counts, void *stream) {
+    DensArgs a;
+    int rc = dens_args(st, a);
+    if (rc) return rc;
+    if (!workspace || !counts) return fail(GSR_ERR_ARG, "densify: null workspace / counts");
+    memset(counts, 0, sizeof(*counts));
+    if (a.P == 0) return GSR_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const DensWorkspace L(a.P);
+    { Phase ph(s, "densify_plan"); HIP_TRY(launch_dens_plan(a, (char *)workspace, s)); }
+    uint32_t tot[4];
+    HIP_TRY(hipMemcpyAsync(tot, (char *)workspace + L.totals, sizeof(tot), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    counts->n_keep_orig = (int)tot[0];
+    counts->n_keep_clone = (int)tot[1];
+    counts->n_split = (int)tot[2];
+    counts->n_keep_split = (int)tot[3];
+    const long long po = (long long)tot[0] + tot[1] + 2ll * tot[3];
+    if (po > 0x7FFFFFFF) return fail(GSR_ERR_UNSUPPORTED, "densify: output too large");
+    counts->P_out = (int)po;
+    return GSR_OK;
+}
+
+int gsr_densify_split_stds(const gsr_densify_settings *st, const void *workspace, float *stds, void *stream) {
+    DensArgs a;
+    int rc = dens_args(st, a);
+    if (rc) return rc;
+    if (a.P == 0) return GSR_OK;
+    if (!workspace || !stds) return fail(GSR_ERR_ARG, "densify: null workspace / stds");
+    HIP_TRY(launch_dens_stds(a, (const char *)workspace, stds, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+int gsr_densify_apply(const gsr_densify_settings *st, const void *workspace, const gsr_densify_counts *counts,
+                      const float *samples, int ncols, const gsr_densify_column *cols, void *stream) {
+    DensArgs a;
+    int rc = dens_args(st, a);
+    if (rc) return rc;
+    if (ncols < 0 || ncols > kDensMaxColumns) return fail(GSR_ERR_ARG, "densify: 0..%d columns", kDensMaxColumns);
+    if (a.P == 0 || ncols == 0) return GSR_OK;
+    if (!workspace || !cols || !counts) return fail(GSR_ERR_ARG, "densify: null workspace / counts / columns");
+    if (counts->n_split > 0 && !samples) return fail(GSR_ERR_ARG, "densify: %d splits need samples", counts->n_split);
+    DensColumns dc;
+    memset(&dc, 0, sizeof(dc));
+    dc.n = ncols;
+    for (int k = 0; k < ncols; ++k) {
+        const gsr_densify_column &c = cols[k];
+        if (c.width <= 0 || !c.src || !c.dst) return fail(GSR_ERR_ARG, "densify: column %d has no data", k);
+        if ((c.exp_avg == nullptr) != (c.exp_avg_sq == nullptr) || (c.exp_avg == nullptr) != (c.dst_exp_avg == nullptr) ||
+            (c.dst_exp_avg == nullptr) != (c.dst_exp_avg_sq == nullptr))
+            return fail(GSR_ERR_ARG, "densify: column %d: Adam moments must be given together", k);
+        if (c.role == GSR_DENS_MEANS && c.width != 3) return fail(GSR_ERR_ARG, "densify: means need width 3");
+        if (c.role == GSR_DENS_LOG_SCALES && c.width != 3) return fail(GSR_ERR_ARG, "densify: log_scales need width 3");
+        dc.c[k] = DensColumn{c.width, c.role, c.src, c.exp_avg, c.exp_avg_sq, c.dst, c.dst_exp_avg, c.dst_exp_avg_sq};
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Phase ph(s, "densify_apply");
+    HIP_TRY(launch_dens_apply(a, (const char *)workspace, samples, dc, s));
+    return GSR_OK;
+}
+
 int gsr_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;

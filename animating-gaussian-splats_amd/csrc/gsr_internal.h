@@ -69,4 +69,30 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float *img1, const fl
                            const float *maps, const float *g_l1, const float *g_ssim, float *dimg1,
                            hipStream_t s);
 
+// densification (gsr_densify.hip)
+struct DensArgs {
+    int P, prune_big;
+    float grad_threshold, small_scale, big_scale, remove_opacity, inv_split_div;
+    const float *grad_accum, *vis_count, *log_scales, *opacity_logits, *rotations;
+};
+struct DensColumn {
+    int width, role;
+    const float *src, *m_src, *v_src;
+    float *dst, *m_dst, *v_dst;
+};
+constexpr int kDensMaxColumns = 8;
+struct DensColumns { int n; DensColumn c[kDensMaxColumns]; };
+struct DensWorkspace {
+    int NB;
+    size_t flags, bsum, boff, totals, total;
+    explicit DensWorkspace(int P);
+};
+hipError_t launch_dens_radii(int P, const int *radii, float *max_radii, uint8_t *visible, hipStream_t s);
+hipError_t launch_dens_grads(int P, const uint8_t *visible, const float *m2grad, float *grad_accum,
+                             float *vis_count, hipStream_t s);
+hipError_t launch_dens_plan(const DensArgs &a, char *ws, hipStream_t s);
+hipError_t launch_dens_stds(const DensArgs &a, const char *ws, float *stds, hipStream_t s);
+hipError_t launch_dens_apply(const DensArgs &a, const char *ws, const float *samples, const DensColumns &cols,
+                             hipStream_t s);
+
 }  // namespace gsr

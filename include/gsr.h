@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 3
+#define GSR_ABI_VERSION 4
 
 enum gsr_status {
     GSR_OK = 0,
@@ -163,6 +163,68 @@ int gsr_l1_ssim_forward(int planes, int height, int width, const float *img1, co
 int gsr_l1_ssim_backward(int planes, int height, int width, const float *img1, const float *img2,
                          const void *scratch, const float *dL_dl1, const float *dL_dssim,
                          float *dL_dimg1, void *stream);
+
+/* ---- Densification: statistics, clone / split / prune with Adam state surgery (ABI >= 4) ------
+ * SURVEY.md 8(f) row 2.  Replaces update_max_2d_radii_and_visibility_mask (densify.py:154-162),
+ * accumulate_mean_2d_gradients (external.py:113-124) and the body of densify_gaussians
+ * (external.py:211-304 with cat_params_to_optimizer / remove_points, :144-204).  All pointers are
+ * device pointers to contiguous fp32 (P, width) rows unless stated. */
+enum gsr_densify_role {
+    GSR_DENS_OTHER = 0,      /* copied to every output row of its Gaussian */
+    GSR_DENS_MEANS = 1,      /* split copies get + build_rotation(q) * sample (external.py:262-265) */
+    GSR_DENS_LOG_SCALES = 2  /* split copies get log(exp(s) / split_divisor) (external.py:266-268) */
+};
+
+typedef struct gsr_densify_settings {
+    int P;
+    float grad_threshold;          /* 0.0002 (external.py:224) */
+    float small_scale;             /* 0.01 * scene_radius: clone if max scale <= it, split if > it */
+    float big_scale;               /* 0.1 * scene_radius: pruned when prune_big (external.py:294-299) */
+    float remove_opacity;          /* sigmoid(logit) below it is pruned: 0.005, or 0.25 at i == 5000 */
+    int prune_big;                 /* i >= 3000 */
+    float split_divisor;           /* 0.8 * n = 1.6 */
+    const float *grad_accum;       /* (P) mean_2d_gradients_accumulated */
+    const float *vis_count;        /* (P) visibility_count */
+    const float *log_scales;       /* (P,3) */
+    const float *opacity_logits;   /* (P,1) */
+    const float *rotation_quaternions; /* (P,4) */
+} gsr_densify_settings;
+
+typedef struct gsr_densify_counts {
+    int n_keep_orig;   /* originals surviving (not split, not pruned) */
+    int n_keep_clone;  /* clones surviving */
+    int n_split;       /* Gaussians split: the reference draws 2 * n_split samples */
+    int n_keep_split;  /* split copies surviving, per copy */
+    int P_out;         /* n_keep_orig + n_keep_clone + 2 * n_keep_split */
+} gsr_densify_counts;
+
+/* One per-Gaussian parameter and its Adam moments (exp_avg / exp_avg_sq may be NULL together when
+ * the optimizer holds no state for it; dst_* likewise).  dst arrays hold P_out rows. */
+typedef struct gsr_densify_column {
+    int width;
+    int role;                      /* gsr_densify_role */
+    const float *src, *exp_avg, *exp_avg_sq;
+    float *dst, *dst_exp_avg, *dst_exp_avg_sq;
+} gsr_densify_column;
+
+/* max_radii[vis] = max(radii, max_radii); visible[i] = radii[i] > 0 (u8). */
+int gsr_densify_update_radii(int P, const int *radii, float *max_radii, uint8_t *visible, void *stream);
+/* grad_accum[vis] += |means2D_grad[vis, :2]|; vis_count[vis] += 1.  means2D_grad is (P,3). */
+int gsr_densify_accumulate_grads(int P, const uint8_t *visible, const float *means2D_grad,
+                                 float *grad_accum, float *vis_count, void *stream);
+size_t gsr_densify_workspace_bytes(int P);
+/* Decides every row's fate and fills *counts (host struct; this call synchronises `stream`, as the
+ * reference's boolean-mask indexing does). */
+int gsr_densify_plan(const gsr_densify_settings *s, void *workspace, gsr_densify_counts *counts,
+                     void *stream);
+/* stds (2 * n_split, 3): exp(log_scales) of the split rows, twice (external.py:257-259) -- the std of
+ * the caller's torch.normal draw. */
+int gsr_densify_split_stds(const gsr_densify_settings *s, const void *workspace, float *stds, void *stream);
+/* Writes every column's P_out output rows (and moments) in the reference's order; `counts` is what
+ * gsr_densify_plan returned, `samples` the (2 * n_split, 3) normal draw (may be NULL when n_split is
+ * 0).  At most 8 columns. */
+int gsr_densify_apply(const gsr_densify_settings *s, const void *workspace, const gsr_densify_counts *counts,
+                      const float *samples, int ncols, const gsr_densify_column *cols, void *stream);
 
 /* Per-phase device timing with HIP events recorded on the call's stream (off by default).
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",

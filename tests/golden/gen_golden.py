@@ -14,8 +14,10 @@ What is captured:
     fused-loss row of SURVEY 8(f))
   * update_max_2d_radii_and_visibility_mask (densify.py:154-162) + accumulate_mean_2d_gradients
     (external.py:113-124) over a sequence of seeded views, and densify_gaussians
-    (external.py:211-314) at i = 500 with a seeded torch.normal - the statistics the data-parallel
-    grad/stat reduction must reproduce.
+    (external.py:211-314) - the statistics the data-parallel grad/stat reduction must reproduce;
+  * densify_gaussians (external.py:211-314) at i = 500 / 3000 / 5000 on a seeded parameter dict with
+    a populated torch Adam (densify.py:68-86): parameters, Adam exp_avg / exp_avg_sq / step and
+    densification statistics before and after, plus the torch.normal split samples it drew.
 
 The reference needs open3d / wandb / imageio / a rasterizer and CUDA; here open3d, wandb and imageio
 are empty stub modules, ``diff_gaussian_rasterization`` is this repo's drop-in (only its settings
@@ -121,7 +123,7 @@ def main():
     loss = 0.8 * l1 + 0.2 * (1.0 - ss)
     loss.backward()
     out["loss_in_img1"], out["loss_in_img2"] = rend.numpy(), seg.numpy()
-    out["loss_out_l1"], out["loss_out_ssim"] = np.array(float(l1)), np.array(float(ss))
+    out["loss_out_l1"], out["loss_out_ssim"] = np.array(l1.item()), np.array(ss.item())
     out["loss_out_grad"] = x.grad.numpy()
 
     # ---- densification statistics over a sequence of views ----------------------------------
@@ -144,6 +146,67 @@ def main():
     out["dstat_out_visibility_count"] = dv.visibility_count.numpy()
     out["dstat_out_grad_accum"] = dv.mean_2d_gradients_accumulated.numpy()
     out["dstat_out_max_radii"] = dv.max_2d_radii.numpy()
+
+    # ---- densify_gaussians (external.py:211-314) with Adam state surgery ------------------------
+    # i = 500: clone / split / prune (opacity < 0.005); i = 3000: + big-point prune and the opacity
+    # reset of external.py:306-314; i = 5000: prune threshold 0.25.  torch.normal is recorded so the
+    # build can be fed the same split samples.
+    real_normal = torch.normal
+    for case, (i_it, seed) in enumerate([(500, 11), (3000, 12), (5000, 13)]):
+        gd = torch.Generator().manual_seed(seed)
+        P, sr = 400, 2.0  # clone/split threshold 0.01 * sr = 0.02, big points > 0.1 * sr = 0.2
+        raw = {"means": torch.randn(P, 3, generator=gd), "colors": torch.rand(P, 3, generator=gd),
+               "segmentation_masks": torch.rand(P, 3, generator=gd),
+               "rotation_quaternions": torch.randn(P, 4, generator=gd),
+               "opacity_logits": 3.0 * torch.randn(P, 1, generator=gd),
+               "log_scales": float(np.log(0.02)) + 0.9 * torch.randn(P, 3, generator=gd),
+               "camera_matrices": torch.zeros(50, 3), "camera_center": torch.zeros(50, 3)}
+        for k, v in raw.items():
+            out[f"dens{case}_in_{k}"] = v.numpy()
+        params = {k: torch.nn.Parameter(v.clone().requires_grad_(True)) for k, v in raw.items()}
+        opt = densify.create_optimizer(params, sr)
+        for _ in range(2):  # populate exp_avg / exp_avg_sq / step
+            for k, p_ in params.items():
+                p_.grad = 0.01 * torch.randn(p_.shape, generator=gd)
+            opt.step()
+        for k, p_ in params.items():
+            st = opt.state[p_]
+            out[f"dens{case}_pre_{k}"] = p_.detach().numpy().copy()
+            out[f"dens{case}_pre_m_{k}"] = st["exp_avg"].numpy().copy()
+            out[f"dens{case}_pre_v_{k}"] = st["exp_avg_sq"].numpy().copy()
+        cnt = torch.randint(0, 5, (P,), generator=gd).float()
+        acc = cnt * 0.0004 * torch.rand(P, generator=gd)
+        dv = shared.DensificationVariables(visibility_count=cnt.clone(), mean_2d_gradients_accumulated=acc.clone(),
+                                           max_2d_radii=torch.randint(0, 9, (P,), generator=gd).float())
+        vis = torch.rand(P, generator=gd) > 0.3
+        m2 = torch.zeros(P, 3, requires_grad=True)
+        m2.grad = 3e-4 * torch.randn(P, 3, generator=gd)
+        dv.gaussian_is_visible_mask, dv.means_2d = vis, m2
+        out[f"dens{case}_in_count"], out[f"dens{case}_in_acc"] = cnt.numpy(), acc.numpy()
+        out[f"dens{case}_in_max_radii"] = dv.max_2d_radii.numpy().copy()
+        out[f"dens{case}_in_vis"], out[f"dens{case}_in_m2grad"] = vis.numpy(), m2.grad.numpy()
+        samples = []
+
+        def recording_normal(*a, **k):
+            r = real_normal(*a, **k)
+            samples.append(r.detach().clone())
+            return r
+        torch.normal = recording_normal
+        torch.manual_seed(100 + case)
+        external.densify_gaussians(params, dv, sr, opt, i_it)
+        torch.normal = real_normal
+        out[f"dens{case}_iter"] = np.array(i_it)
+        out[f"dens{case}_scene_radius"] = np.array(sr)
+        out[f"dens{case}_samples"] = (samples[0].numpy() if samples else np.zeros((0, 3), np.float32))
+        for k, p_ in params.items():
+            st = opt.state[p_]
+            out[f"dens{case}_out_{k}"] = p_.detach().numpy()
+            out[f"dens{case}_out_m_{k}"] = st["exp_avg"].numpy()
+            out[f"dens{case}_out_v_{k}"] = st["exp_avg_sq"].numpy()
+            out[f"dens{case}_out_step_{k}"] = np.array(float(st["step"]))
+        out[f"dens{case}_out_count"] = dv.visibility_count.numpy()
+        out[f"dens{case}_out_acc"] = dv.mean_2d_gradients_accumulated.numpy()
+        out[f"dens{case}_out_max_radii"] = dv.max_2d_radii.numpy()
 
     np.savez_compressed(os.path.join(HERE, "reference_harness.npz"), **out)
     print(f"wrote {len(out)} arrays to tests/golden/reference_harness.npz")
