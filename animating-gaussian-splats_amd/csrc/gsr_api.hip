@@ -489,6 +489,58 @@ int gsr_densify_apply(const gsr_densify_settings *st, const void *workspace, con
     return GSR_OK;
 }
 
+int gsr_adam_step(int ntensors, const gsr_adam_tensor *tensors, double beta1, double beta2, double eps,
+                  void *stream) {
+    if (ntensors < 0 || (ntensors > 0 && !tensors)) return fail(GSR_ERR_ARG, "adam: bad tensor list");
+    hipStream_t s = (hipStream_t)stream;
+    for (int k = 0; k < ntensors; ++k) {  // validate everything before launching anything
+        const gsr_adam_tensor &a = tensors[k];
+        if (a.numel < 0) return fail(GSR_ERR_ARG, "adam: tensor %d: negative numel", k);
+        if (a.numel > 0 && (!a.param || !a.grad || !a.exp_avg || !a.exp_avg_sq))
+            return fail(GSR_ERR_ARG, "adam: tensor %d: null pointer", k);
+        if (a.numel > 0 && !(a.step >= 1.0)) return fail(GSR_ERR_ARG, "adam: tensor %d: step must be >= 1", k);
+        if (adam_blocks(a.numel) > (1 << 30)) return fail(GSR_ERR_UNSUPPORTED, "adam: tensor %d too large", k);
+    }
+    Phase ph(s, "adam");
+    AdamTable tab;
+    auto reset = [&]() {
+        memset(&tab, 0, sizeof(tab));
+        tab.w1 = (float)(1.0 - beta1);
+        tab.b2 = (float)beta2;
+        tab.omb2 = (float)(1.0 - beta2);
+        tab.eps = (float)eps;
+    };
+    reset();
+    int nb = 0;
+    for (int k = 0; k < ntensors; ++k) {
+        const gsr_adam_tensor &a = tensors[k];
+        if (a.numel == 0) continue;
+        const int b = adam_blocks(a.numel);
+        if (tab.n == kAdamMaxTensors || nb + (long long)b > (1ll << 30)) {  // table full: launch it
+            tab.block_start[tab.n] = nb;
+            HIP_TRY(launch_adam(tab, s));
+            reset();
+            nb = 0;
+        }
+        const double bc1 = 1.0 - std::pow(beta1, a.step), bc2 = 1.0 - std::pow(beta2, a.step);
+        AdamTensor &t = tab.t[tab.n];
+        t.param = a.param; t.grad = a.grad; t.exp_avg = a.exp_avg; t.exp_avg_sq = a.exp_avg_sq;
+        t.n = a.numel;
+        t.step_size = (float)((a.lr / bc1) * -1.0);
+        t.bc2_sqrt = (float)std::pow(bc2, 0.5);
+        const uintptr_t al = (uintptr_t)a.param | (uintptr_t)a.grad | (uintptr_t)a.exp_avg | (uintptr_t)a.exp_avg_sq;
+        t.vec4 = (al & 15) == 0;
+        tab.block_start[tab.n] = nb;
+        nb += b;
+        ++tab.n;
+    }
+    if (tab.n) {
+        tab.block_start[tab.n] = nb;
+        HIP_TRY(launch_adam(tab, s));
+    }
+    return GSR_OK;
+}
+
 int gsr_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;

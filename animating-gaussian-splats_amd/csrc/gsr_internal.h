@@ -95,4 +95,18 @@ hipError_t launch_dens_stds(const DensArgs &a, const char *ws, float *stds, hipS
 hipError_t launch_dens_apply(const DensArgs &a, const char *ws, const float *samples, const DensColumns &cols,
                              hipStream_t s);
 
+// fused Adam (gsr_adam.hip)
+struct AdamTensor {
+    float *param; const float *grad; float *exp_avg; float *exp_avg_sq;
+    long long n; float step_size, bc2_sqrt; int vec4;
+};
+constexpr int kAdamMaxTensors = 16;
+struct AdamTable {
+    int n; float w1, b2, omb2, eps;
+    AdamTensor t[kAdamMaxTensors];
+    int block_start[kAdamMaxTensors + 1];
+};
+int adam_blocks(long long n);
+hipError_t launch_adam(const AdamTable &tab, hipStream_t s);
+
 }  // namespace gsr

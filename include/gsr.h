@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 4
+#define GSR_ABI_VERSION 5
 
 enum gsr_status {
     GSR_OK = 0,
@@ -226,9 +226,27 @@ int gsr_densify_split_stds(const gsr_densify_settings *s, const void *workspace,
 int gsr_densify_apply(const gsr_densify_settings *s, const void *workspace, const gsr_densify_counts *counts,
                       const float *samples, int ncols, const gsr_densify_column *cols, void *stream);
 
+/* ---- Fused Adam step over the per-Gaussian parameters (ABI >= 5) ---------
+ * Replaces optimizer.step() of torch.optim.Adam(..., eps=1e-15) (densify.py:68-86, :247) for every
+ * tensor in one launch, with torch's _multi_tensor_adam operation order.  `step` is the tensor's
+ * step count after this update (torch increments it first); lr / step / betas / eps are the group's
+ * Python values (bias corrections are formed in double, as torch does). */
+typedef struct gsr_adam_tensor {
+    float *param;
+    const float *grad;
+    float *exp_avg;
+    float *exp_avg_sq;
+    long long numel;
+    double lr;
+    double step;
+} gsr_adam_tensor;
+
+int gsr_adam_step(int ntensors, const gsr_adam_tensor *tensors, double beta1, double beta2, double eps,
+                  void *stream);
+
 /* Per-phase device timing with HIP events recorded on the call's stream (off by default).
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
- * "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd".  gsr_profile_read synchronises on the recorded events. */
+ * "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam".  gsr_profile_read synchronises on the recorded events. */
 int gsr_profile_enable(int on);
 /* Restrict event recording to a comma-separated list of phases (NULL or "" = every phase), so a
  * timed region can carry the events of one kernel only.  Host-side timers are unaffected. */
