@@ -135,6 +135,151 @@ def loss_call_site(steps, cam, leaves, dev):
             "ssim_bwd_GBps": round(24 * n / (kms["ssim_bwd"] * 1e-3) / 1e9, 1), "steps": steps}
 
 
+def _torch_densify_event(params, acc, cnt, scene_radius, opt, i):
+    """external.py:211-304's densification as the reference composes it from torch ops (the
+    comparison leg only): clone, split with torch.normal, drop split originals, prune, Adam surgery."""
+    keys = [k for k in params if k not in ("camera_matrices", "camera_center")]
+
+    def swap(new):  # cat_params_to_optimizer / remove_points: new tensor + moments per parameter
+        for k, (v, m, s2) in new.items():
+            grp = [g for g in opt.param_groups if g["name"] == k][0]
+            st = opt.state.pop(grp["params"][0], None)
+            p = torch.nn.Parameter(v.requires_grad_(True))
+            if st is not None:
+                st["exp_avg"], st["exp_avg_sq"] = m, s2
+                opt.state[p] = st
+            grp["params"][0] = params[k] = p
+
+    def moments(k):
+        st = opt.state.get([g for g in opt.param_groups if g["name"] == k][0]["params"][0], {})
+        return st.get("exp_avg"), st.get("exp_avg_sq")
+
+    avg = acc / cnt
+    avg[avg.isnan()] = 0.0
+    ms = torch.exp(params["log_scales"]).max(dim=1).values
+    clone = (avg >= 0.0002) & (ms <= 0.01 * scene_radius)
+    swap({k: (torch.cat((params[k], params[k][clone])),
+              *[torch.cat((t, torch.zeros_like(params[k][clone]))) if t is not None else None for t in moments(k)])
+          for k in keys})
+    n = params["means"].shape[0]
+    pad = torch.zeros(n, device=avg.device)
+    pad[:avg.shape[0]] = avg
+    split = (pad >= 0.0002) & (torch.exp(params["log_scales"]).max(dim=1).values > 0.01 * scene_radius)
+    new = {k: params[k][split].repeat(2, 1) for k in keys}
+    stds = torch.exp(params["log_scales"])[split].repeat(2, 1)
+    samples = torch.normal(mean=torch.zeros((stds.size(0), 3), device=stds.device), std=stds)
+    q = torch.nn.functional.normalize(params["rotation_quaternions"][split])
+    r, x, y, z = q.unbind(-1)
+    R = torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                     2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                     2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], -1).view(-1, 3, 3)
+    new["means"] = new["means"] + torch.bmm(R.repeat(2, 1, 1), samples.unsqueeze(-1)).squeeze(-1)
+    new["log_scales"] = torch.log(torch.exp(new["log_scales"]) / 1.6)
+    swap({k: (torch.cat((params[k], new[k])),
+              *[torch.cat((t, torch.zeros_like(new[k]))) if t is not None else None for t in moments(k)])
+          for k in keys})
+    keep = ~torch.cat((split, torch.zeros(new["means"].shape[0], dtype=torch.bool, device=split.device)))
+    swap({k: (params[k][keep], *[t[keep] if t is not None else None for t in moments(k)]) for k in keys})
+    keep = ~(torch.sigmoid(params["opacity_logits"]) < 0.005).squeeze()
+    swap({k: (params[k][keep], *[t[keep] if t is not None else None for t in moments(k)]) for k in keys})
+
+
+def densify_call_site(steps, cfg, cam, dev):
+    """densify.py's loop body (densify.py:234-258) at the bench resolution on a 1M-Gaussian
+    densify.py-style parameter dict: (a) the native path (splat_train.densify_iteration: fused
+    activations, fused L1+SSIM, statistics kernels, FusedAdam) vs (b) the reference's composition
+    (torch activations + this rasterizer + torch calc_ssim / l1 + torch statistics + torch.optim.Adam),
+    ms per iteration; and one densification event (clone / split / prune + Adam surgery) each way."""
+    import splat_adam
+    import splat_densify
+    import splat_scenes as S
+    import splat_train
+    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    P = cfg.P
+    g = torch.Generator().manual_seed(7)
+    base = S.synthetic_cloud(P, cfg.s0, seed=0, device="cpu")
+    base["segmentation_masks"] = (torch.rand(P, 1, generator=g) > 0.5).float().repeat(1, 3)
+    base["camera_matrices"] = torch.zeros(50, 3)
+    base["camera_center"] = torch.zeros(50, 3)
+    order = ["means", "colors", "segmentation_masks", "rotation_quaternions", "opacity_logits", "log_scales",
+             "camera_matrices", "camera_center"]
+    lrs = {"means": 0.00016 * 4.0, "colors": 0.0025, "segmentation_masks": 0.0, "rotation_quaternions": 0.001,
+           "opacity_logits": 0.05, "log_scales": 0.001, "camera_matrices": 1e-4, "camera_center": 1e-4}
+    H, W = cfg.height, cfg.width
+    view = splat_train.View(0, cam, torch.rand(3, H, W, generator=g).to(dev),
+                            (torch.rand(1, H, W, generator=g) > 0.5).float().repeat(3, 1, 1).to(dev))
+
+    def fresh(opt_cls):
+        params = {k: torch.nn.Parameter(base[k].to(dev).contiguous()) for k in order}
+        opt = opt_cls([{"params": [params[k]], "name": k, "lr": lrs[k]} for k in order], lr=0.0, eps=1e-15)
+        return params, opt, splat_train.create_densification_variables(params)
+
+    def native(state, i):
+        params, opt, dv = state
+        splat_train.densify_iteration(params, view, dv, opt, 4.0, i)
+
+    def reference(state, i):
+        params, opt, dv = state
+        ra = S.render_arguments(params)
+        ra["means2D"].retain_grad()
+        img, radii, _ = GaussianRasterizer(raster_settings=cam)(**ra)
+        li = 0.8 * torch.nn.functional.l1_loss(img, view.image) + 0.2 * (1.0 - _torch_calc_ssim(img, view.image))
+        rs = S.render_arguments(params)
+        rs["colors_precomp"] = params["segmentation_masks"]
+        seg, _, _ = GaussianRasterizer(raster_settings=cam)(**rs)
+        ls = 0.8 * torch.nn.functional.l1_loss(seg, view.segmentation_mask) + \
+            0.2 * (1.0 - _torch_calc_ssim(seg, view.segmentation_mask))
+        pos = radii > 0
+        dv.max_2d_radii[pos] = torch.max(radii[pos], dv.max_2d_radii[pos])
+        (li + 3 * ls).backward()
+        with torch.no_grad():
+            dv.mean_2d_gradients_accumulated[pos] += torch.norm(ra["means2D"].grad[pos, :2], dim=-1)
+            dv.visibility_count[pos] += 1
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+
+    def timed(fn, state, first):
+        for i in range(2):
+            fn(state, first + i)  # warm-up (off the densify schedule: i % 100 != 0)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(steps):
+            fn(state, first + 2 + i)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / steps * 1e3
+
+    nat_state = fresh(splat_adam.FusedAdam)
+    nat = timed(native, nat_state, 501)
+    ref_state = fresh(torch.optim.Adam)
+    ref = timed(reference, ref_state, 501)
+    # one densification event each way, on the statistics the timed iterations accumulated
+    out = {"gaussians": P, "image": f"{W}x{H}", "native_iteration_ms": round(nat, 3),
+           "reference_composition_iteration_ms": round(ref, 3), "steps": steps}
+    for name, state in (("native", nat_state), ("reference", ref_state)):
+        params, opt, dv = state
+        acc, cnt = dv.mean_2d_gradients_accumulated.clone(), dv.visibility_count.clone()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        if name == "native":
+            _C.profile_reset()
+            _C.profile_select(["densify_plan", "densify_apply"])
+            _C.profile_enable(True)
+            dv.mean_2d_gradients_accumulated, dv.visibility_count = acc, cnt
+            info = splat_densify._densify(params, dv, 4.0, opt, 600, None)
+        else:
+            _torch_densify_event(params, acc, cnt, 4.0, opt, 600)
+        torch.cuda.synchronize()
+        out[f"{name}_densify_event_ms"] = round((time.perf_counter() - t) * 1e3, 3)
+        if name == "native":
+            _C.profile_enable(False)
+            apply_ms = _C.profile_read("densify_apply")[0]
+            _C.profile_select(None)
+            out["densify_rows"] = info
+            # apply: every input row read (17 floats x param + 2 moments) + every output row written
+            out["densify_apply_GBps"] = round(4 * 17 * 3 * (P + info["P_out"]) / (apply_ms * 1e-3) / 1e9, 1)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -147,6 +292,8 @@ def main():
                     help="steps timed for each train.py call-site variant (0 = skip)")
     ap.add_argument("--loss-steps", type=int, default=10,
                     help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip)")
+    ap.add_argument("--densify-steps", type=int, default=5,
+                    help="densify.py iterations timed per variant at the bench resolution (0 = skip)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="untimed steps with events on every phase (per-kernel breakdown)")
     args = ap.parse_args()
@@ -275,6 +422,7 @@ def main():
                      "steps": args.call_site_steps}
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
     loss_site = loss_call_site(args.loss_steps, cams[0], leaves, dev) if args.loss_steps > 0 else None
+    dens_site = densify_call_site(args.densify_steps, cfg, cams[0], dev) if args.densify_steps > 0 else None
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
     import splat_dp
     used = sorted({ci for it in range(args.warmup + args.probe_steps, args.warmup + args.probe_steps + args.steps)
@@ -337,6 +485,7 @@ def main():
             "cpu_baseline": cpu,
             "call_site": call_site,
             "loss_call_site": loss_site,
+            "densify_call_site": dens_site,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:
