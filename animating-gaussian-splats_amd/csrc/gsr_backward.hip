@@ -526,12 +526,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
     const int nrow = min(kShBlock, P - i0);
-    if (MC > 0) {  // coalesced copy of this block's SH rows into LDS (reused for dL/dSH)
-        const float *src = shs + (size_t)i0 * RL;
-        for (int e = threadIdx.x; e < nrow * RL; e += kShBlock) {
-            const int r = e / RL;
-            s_sh[r * RS + (e - r * RL)] = src[e];
-        }
+    if constexpr (MC > 0) {  // coalesced copy of this block's SH rows into LDS (reused for dL/dSH)
+        sh_rows_to_lds<MC>(shs + (size_t)i0 * RL, nrow, s_sh);
         __syncthreads();
     }
     const int i = i0 + threadIdx.x;
@@ -540,13 +536,9 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
                                  radii, goff, part, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
                                  act, rec);
-    if (MC > 0) {  // coalesced store of the dL/dSH rows
+    if constexpr (MC > 0) {  // coalesced store of the dL/dSH rows
         __syncthreads();
-        float *dst = dL_dsh + (size_t)i0 * RL;
-        for (int e = threadIdx.x; e < nrow * RL; e += kShBlock) {
-            const int r = e / RL;
-            dst[e] = s_sh[r * RS + (e - r * RL)];
-        }
+        sh_rows_from_lds<MC>(s_sh, nrow, dL_dsh + (size_t)i0 * RL);
     }
 }
 

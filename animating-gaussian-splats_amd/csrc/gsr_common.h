@@ -121,6 +121,77 @@ struct ScratchLayout {
 constexpr int kShBlock = 256;
 __host__ __device__ constexpr int sh_row_stride(int MC) { return (3 * MC) | 1; }  // odd: no bank conflicts
 
+// Block copy of `nrow` SH rows (3 MC floats each, contiguous in global memory) into LDS rows of
+// stride sh_row_stride(MC).  The block's global span starts 16-byte aligned whenever the array does
+// (kShBlock * 3 MC is a multiple of 4), so it is read as float4: every thread issues all its loads
+// before its first LDS store (up to 12 in flight per lane for MC = 16).
+template <int MC>
+__device__ inline void sh_rows_to_lds(const float *__restrict__ src, int nrow, float *s) {
+    constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
+    constexpr int IT = (kShBlock * RL / 4 + kShBlock - 1) / kShBlock;
+    const int n = nrow * RL;
+    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        const int n4 = n >> 2;
+        const float4 *s4 = reinterpret_cast<const float4 *>(src);
+        float4 v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int q = threadIdx.x + it * kShBlock;
+            if (q < n4) v[it] = s4[q];
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int q = threadIdx.x + it * kShBlock;
+            if (q < n4) {
+                const float f[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = 4 * q + j, r = e / RL;
+                    s[r * RS + (e - r * RL)] = f[j];
+                }
+            }
+        }
+        for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += kShBlock) {
+            const int r = e / RL;
+            s[r * RS + (e - r * RL)] = src[e];
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += kShBlock) {
+            const int r = e / RL;
+            s[r * RS + (e - r * RL)] = src[e];
+        }
+    }
+}
+
+// The reverse copy (LDS rows -> contiguous global rows), float4 stores when aligned.
+template <int MC>
+__device__ inline void sh_rows_from_lds(const float *s, int nrow, float *__restrict__ dst) {
+    constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
+    const int n = nrow * RL;
+    if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
+        const int n4 = n >> 2;
+        float4 *d4 = reinterpret_cast<float4 *>(dst);
+        for (int q = threadIdx.x; q < n4; q += kShBlock) {
+            float f[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int e = 4 * q + j, r = e / RL;
+                f[j] = s[r * RS + (e - r * RL)];
+            }
+            d4[q] = make_float4(f[0], f[1], f[2], f[3]);
+        }
+        for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += kShBlock) {
+            const int r = e / RL;
+            dst[e] = s[r * RS + (e - r * RL)];
+        }
+    } else {
+        for (int e = threadIdx.x; e < n; e += kShBlock) {
+            const int r = e / RL;
+            dst[e] = s[r * RS + (e - r * RL)];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Device math -- same op order as oracle/gsr_oracle.c
 // ---------------------------------------------------------------------------------------------

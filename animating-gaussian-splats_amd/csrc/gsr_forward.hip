@@ -38,13 +38,8 @@ __global__ __launch_bounds__(256) void k_preprocess(
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
-    if (MC > 0) {  // coalesced copy of this block's SH rows into LDS
-        const int nrow = min(kShBlock, P - i0);
-        const float *src = shs + (size_t)i0 * RL;
-        for (int e = threadIdx.x; e < nrow * RL; e += kShBlock) {
-            const int r = e / RL;
-            s_sh[r * RS + (e - r * RL)] = src[e];
-        }
+    if constexpr (MC > 0) {  // coalesced copy of this block's SH rows into LDS
+        sh_rows_to_lds<MC>(shs + (size_t)i0 * RL, min(kShBlock, P - i0), s_sh);
         __syncthreads();
     }
     const int i = i0 + threadIdx.x;
