@@ -34,7 +34,7 @@ __global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *
 // 4 independent tiles per 256-thread block, dispatched by descending work (tile_order).
 // Per surviving (tile, Gaussian) pair each contributing pixel adds s = dL/dG * G times
 // (dx, dy, dx^2, dx dy, dy^2) plus dL/dopacity and dL/dcolour terms; the lane sums its 4 pixels
-// in registers, the wave folds the 9 sums with permlane swaps + DPP (wave_sum9), and at the end of
+// in registers, the wave reduces them with permlane swaps + DPP (wave_pair_sums), and at the end of
 // the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
 // quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour)
 // with the exact conic, storing one 36-byte record per sorted slot (coalesced, no atomics).
@@ -107,7 +107,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         AR[k] = bd;
     }
     const int row = lane >> 4;
-    const int slot0123 = (row == 0) ? 0 : (row == 1) ? 2 : (row == 2) ? 1 : 3;  // wave_sum9 lane map
+    // s_out slots per pair: 0 sum dx S0, 1 sum S1, 2 sum dx^2 S0, 3 sum dx S1, 4 sum S4, 5 sum S0,
+    // 6..8 sum cs (the first five still to be scaled by the opacity); wave_pair_sums row map:
+    const int xslot = (row == 0) ? 0 : (row == 1) ? 4 : (row == 2) ? 1 : 6;
+    const int yslot = (row == 0) ? 2 : (row == 1) ? 7 : (row == 2) ? 3 : 8;
     for (int end = maxc; end > 0; end -= 64) {
         const int start = end > 64 ? end - 64 : 0;
         const int cnt = end - start;
@@ -174,13 +177,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(
                 cs2 = fmaf(dch, dp2[k], cs2);
             }
             if (__ballot(any)) {
-                // moments of sG = opacity * G * dL/dalpha: (dx, dy, dx^2, dx dy, dy^2)
-                const float v0 = (b.y * x.dx) * S0, v1 = b.y * S1;
-                const Sum9 sm = wave_sum9(v0, v1, x.dx * v0, x.dx * v1, b.y * S4, S0, cs0, cs1, cs2);
+                // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
+                const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
                 if ((lane & 15) == 0) {
-                    s_out[j * kPartial + slot0123] = sm.r0123;
-                    s_out[j * kPartial + 4 + slot0123] = sm.r4567;
-                    if (lane == 0) s_out[j * kPartial + 8] = sm.r8;
+                    s_out[j * kPartial + xslot] = sm.X;
+                    s_out[j * kPartial + yslot] = sm.Y;
+                    if (lane == 0) s_out[j * kPartial + 5] = sm.Z;
                 }
             }
         }
@@ -189,13 +191,14 @@ __global__ __launch_bounds__(256) void k_render_bwd(
             const float4 cj = rec[(size_t)kRecF4 * g_st + 3];  // exact conic (a, b, c)
             const uint32_t em = slot_emit[rg.x + start + lane];
             const float *sm = s_out + lane * kPartial;
-            const float S1 = sm[0], S2 = sm[1];
+            const float o = s_b[lane].y;  // the moments of sG = opacity G dL/dalpha
+            const float S1 = o * sm[0], S2 = o * sm[1];
             float4 *dst = part + 3 * (size_t)em;
             dst[0] = make_float4((-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
                                  (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
-                                 -0.5f * sm[2],                       // dL/dconic.a
-                                 -0.5f * sm[3]);                      // dL/dconic.b (b/2 convention)
-            dst[1] = make_float4(-0.5f * sm[4], sm[5], sm[6], sm[7]);  // dconic.c, dopacity, dcolour.rg
+                                 -0.5f * (o * sm[2]),                 // dL/dconic.a
+                                 -0.5f * (o * sm[3]));                // dL/dconic.b (b/2 convention)
+            dst[1] = make_float4(-0.5f * (o * sm[4]), sm[5], sm[6], sm[7]);  // dconic.c, dopacity, dcolour.rg
             dst[2] = make_float4(sm[8], 0.f, 0.f, 0.f);                // dcolour.b
         }
     }

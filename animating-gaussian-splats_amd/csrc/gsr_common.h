@@ -533,6 +533,29 @@ __device__ inline float row_sum16(float v) {  // every lane of each 16-lane row 
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
     return v;
 }
+// Per-pair gradient sums of the backward blend (k_render_bwd): each lane holds, for its 4 pixels of
+// one column, S0 = sum sG, S1 = sum sG dy, S4 = sum sG dy^2 and cs_c = sum alpha T dL/dpix_c.  The 9
+// wave sums the record needs are sum S0, sum dx S0, sum dx^2 S0, sum S1, sum dx S1, sum S4, sum cs_c
+// with dx = the column's offset, so the rows of a column are folded FIRST (3 + 2 permlane swaps on
+// the 6 raw values instead of 5 + 3 on 9 weighted ones), the column weights dx, dx^2 applied to the
+// column sums, and each 16-lane row summed with DPP.  Totals (every lane of a row holds its row's):
+//   X rows: [sum dx S0, sum S4, sum S1, sum cs0]    Y rows: [sum dx^2 S0, sum cs1, sum dx S1, sum cs2]
+//   Z row 0: sum S0
+struct PairSums { float X, Y, Z; };
+__device__ inline PairSums wave_pair_sums(float S0, float S1, float S4, float cs0, float cs1, float cs2,
+                                          float dx, int row) {
+    const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(cs1, cs2);
+    const float rA = fold16(pA, pB);   // column sums, rows [S0, S4, S1, cs0]
+    const float rC = fold16(0.f, pC);  // rows [0, cs1, 0, cs2]
+    const float wx = row == 0 ? dx : 1.f;
+    const float wy = row == 0 ? dx * dx : (row == 2 ? dx : 0.f);
+    PairSums r;
+    r.X = row_sum16(rA * wx);
+    r.Y = row_sum16(fmaf(rA, wy, rC));
+    r.Z = row_sum16(rA);
+    return r;
+}
+
 struct Sum9 { float r0123, r4567, r8; };
 __device__ inline Sum9 wave_sum9(float v0, float v1, float v2, float v3, float v4, float v5, float v6,
                                  float v7, float v8) {
