@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
     float4 *__restrict__ part) {
     __shared__ float4 s_rec[kTilesPerBlock][3][64];
-    __shared__ float s_outs[kTilesPerBlock][64 * kPartial];
+    __shared__ float s_outs[kTilesPerBlock][64 * 2 * kPartial];  // two halves per sum
     __shared__ uint32_t s_qs[kTilesPerBlock][64];
     const int wv = threadIdx.x >> 6;
     const int t_lin = blockIdx.x * kTilesPerBlock + wv;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         const int start = end > 64 ? end - 64 : 0;
         const int cnt = end - start;
 #pragma unroll
-        for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
+        for (int q = 0; q < 2 * kPartial; ++q) s_out[lane * 2 * kPartial + q] = 0.f;
         // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile; a
         // quarter whose pixels all precede this slot in the forward's order (p >= its max
         // n_contrib) is skipped too
@@ -179,10 +179,11 @@ __global__ __launch_bounds__(256) void k_render_bwd(
             if (__ballot(any)) {
                 // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
                 const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
-                if ((lane & 15) == 0) {
-                    s_out[j * kPartial + xslot] = sm.X;
-                    s_out[j * kPartial + yslot] = sm.Y;
-                    if (lane == 0) s_out[j * kPartial + 5] = sm.Z;
+                if ((lane & 15) < 2) {  // lanes 0 and 1 of each row: the two halves of its sums
+                    float *o2 = s_out + j * 2 * kPartial + (lane & 1);
+                    o2[2 * xslot] = sm.X;
+                    o2[2 * yslot] = sm.Y;
+                    if (lane < 2) o2[2 * 5] = sm.Z;
                 }
             }
         }
@@ -190,7 +191,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         if (lane < cnt) {
             const float4 cj = rec[(size_t)kRecF4 * g_st + 3];  // exact conic (a, b, c)
             const uint32_t em = slot_emit[rg.x + start + lane];
-            const float *sm = s_out + lane * kPartial;
+            const float *s2 = s_out + lane * 2 * kPartial;
+            float sm[kPartial];
+#pragma unroll
+            for (int q = 0; q < kPartial; ++q) sm[q] = s2[2 * q] + s2[2 * q + 1];
             const float o = s_b[lane].y;  // the moments of sG = opacity G dL/dalpha
             const float S1 = o * sm[0], S2 = o * sm[1];
             float4 *dst = part + 3 * (size_t)em;

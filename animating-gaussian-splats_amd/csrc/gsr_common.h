@@ -533,12 +533,23 @@ __device__ inline float row_sum16(float v) {  // every lane of each 16-lane row 
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
     return v;
 }
+// Three of the four row_sum16 stages: lane l of a row ends with the sum over the row's lanes of l's
+// parity, so lanes 0 and 1 of each row hold the two halves of the row total (the last DPP stage, a
+// quad_perm that compiles to a DPP move + add, is left to the consumer's single add).
+__device__ inline float row_sum16_pairs(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+    return v;
+}
+
 // Per-pair gradient sums of the backward blend (k_render_bwd): each lane holds, for its 4 pixels of
 // one column, S0 = sum sG, S1 = sum sG dy, S4 = sum sG dy^2 and cs_c = sum alpha T dL/dpix_c.  The 9
 // wave sums the record needs are sum S0, sum dx S0, sum dx^2 S0, sum S1, sum dx S1, sum S4, sum cs_c
 // with dx = the column's offset, so the rows of a column are folded FIRST (3 + 2 permlane swaps on
 // the 6 raw values instead of 5 + 3 on 9 weighted ones), the column weights dx, dx^2 applied to the
-// column sums, and each 16-lane row summed with DPP.  Totals (every lane of a row holds its row's):
+// column sums, and each 16-lane row summed with DPP to two halves (row_sum16_pairs: lanes 0 and 1 of
+// a row hold them).  Row totals:
 //   X rows: [sum dx S0, sum S4, sum S1, sum cs0]    Y rows: [sum dx^2 S0, sum cs1, sum dx S1, sum cs2]
 //   Z row 0: sum S0
 struct PairSums { float X, Y, Z; };
@@ -550,9 +561,9 @@ __device__ inline PairSums wave_pair_sums(float S0, float S1, float S4, float cs
     const float wx = row == 0 ? dx : 1.f;
     const float wy = row == 0 ? dx * dx : (row == 2 ? dx : 0.f);
     PairSums r;
-    r.X = row_sum16(rA * wx);
-    r.Y = row_sum16(fmaf(rA, wy, rC));
-    r.Z = row_sum16(rA);
+    r.X = row_sum16_pairs(rA * wx);
+    r.Y = row_sum16_pairs(fmaf(rA, wy, rC));
+    r.Z = row_sum16_pairs(rA);
     return r;
 }
 
