@@ -37,6 +37,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh), corrected
 # per MI355X_MICROARCH.md (2 x FETCH_SIZE + WRITE_SIZE): HBM bytes per launch of each kernel
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_hbm_pmc.json")
+# SQ counters of the same command (tools/profile_round.sh sq passes): VALU activity per launch
+SQ_SUMMARY = os.path.join(REPO, "profiles", "r01_sq_pmc.json")
+VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
 PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "render_bwd",
           "gauss_bwd"]
 
@@ -452,6 +455,20 @@ def main():
         pm = json.load(open(PMC_SUMMARY)).get("k_" + dom)
         if pm:
             traffic = int(pm["hbm_bytes_per_launch_corrected"])
+    valu = None
+    if os.path.exists(SQ_SUMMARY):
+        q = json.load(open(SQ_SUMMARY)).get("k_" + dom)
+        if q and "SQ_INSTS_VALU" in q:
+            # the kernel's wave64 VALU instructions (profile of this command) over its live duration,
+            # vs one per 2 cycles on every SIMD (the v_fma_f32 rate; transcendentals, DPP and permlane
+            # ops occupy the pipe 2-4x longer: tools/valu_rate_probe.hip), so issue_frac is a floor
+            # on the VALU pipe's busy share
+            rate = q["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
+            valu = {"insts_per_launch": int(q["SQ_INSTS_VALU"]),
+                    "trans_insts_per_launch": int(q.get("SQ_INSTS_VALU_TRANS_F32", 0)),
+                    "achieved_Ginst_s": round(rate, 1), "peak_Ginst_s": VALU_PEAK_GINST,
+                    "issue_frac": round(rate / VALU_PEAK_GINST, 4),
+                    "source": os.path.relpath(SQ_SUMMARY, REPO)}
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, cfg.sh_degree >= 0)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
 
@@ -479,7 +496,8 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
                          "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if traffic else None,
-                         "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch)},
+                         "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch),
+                         "valu": valu},
             "phase_ms_per_launch": {ph: round(probe[ph][0] / max(probe[ph][1], 1), 5) for ph in PHASES},
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,

@@ -1,9 +1,10 @@
 #!/bin/bash
 # Profile bench.py with rocprofv3 on the GPU box: kernel trace + stats, then the HBM counters in
-# two separate PMC passes (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950).  Same bench
+# two separate PMC passes (FETCH_SIZE and WRITE_SIZE do not fit one pass on gfx950), then two
+# passes of SQ counters (VALU / LDS / SALU activity) for the compute-bound kernels.  Same bench
 # arguments in every pass, so the per-launch averages describe the command bench.py reports on.
 # usage (on the box, from the repo root): bash tools/profile_round.sh <tag> [bench args...]
-# outputs: gpurun_out/prof_<tag>/{trace,fetch,write}/ raw CSV, trace_summary.txt, hbm_pmc.json
+# outputs: gpurun_out/prof_<tag>/{trace,fetch,write,sq1,sq2}/ raw CSV, trace_summary.txt, hbm_pmc.json, sq_pmc.json
 set -u
 tag=${1:-r01}; shift || true
 R=$(pwd)
@@ -19,8 +20,16 @@ echo "fetch ok"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/write" -- \
     python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 3; }
 echo "write ok"
+for pass in 1 2; do
+  if [ $pass = 1 ]; then CTR="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT";
+  else CTR="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_WAIT_ANY SQ_INSTS_VALU_TRANS_F32"; fi
+  timeout -k 10 400 rocprofv3 --pmc $CTR --kernel-include-regex "render|gauss_bwd|preprocess|bin_emit" --kernel-trace --output-format csv -d "$O/sq$pass" -- \
+      python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/sq$pass.log" 2>&1 || { echo "sq pass $pass failed rc=$?"; exit 4; }
+done
+echo "sq ok"
 cd "$R"
 python3 tools/rocprof_summary.py trace "$O/trace" --last 20 --out "$O/trace_summary.json" > "$O/trace_summary.txt"
 python3 tools/rocprof_summary.py pmc "$O/fetch" "$O/write" --out "$O/hbm_pmc.json" > "$O/hbm_pmc.txt"
+python3 tools/rocprof_summary.py sq "$O/sq1" "$O/sq2" --out "$O/sq_pmc.json" > "$O/sq_pmc.txt"
 cp "$O"/trace/*/*_kernel_stats.csv "$O/kernel_stats.csv" 2>/dev/null || true
 echo "summaries ok"

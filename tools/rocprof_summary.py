@@ -5,6 +5,10 @@ Usage:
         -> per-kernel calls / avg / total us (+ average of the last N launches = bench's timed steps)
   python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> [--out profiles/x.json]
         -> per-kernel avg FETCH_SIZE / WRITE_SIZE per launch and corrected HBM bytes
+  python tools/rocprof_summary.py sq     <dir> [<dir> ...] [--out profiles/x.json]
+        -> per-kernel avg of every SQ counter per launch (tools/pmc_stall.sh passes), the launches'
+           avg duration in those passes, and the VALU instruction-issue fraction
+           SQ_INSTS_VALU / (duration x 1024 SIMDs x 2.4 GHz / 2 cycles)
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KiB) reports exactly half the
 bytes of a wide coalesced streaming read, so HBM read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is
@@ -62,6 +66,25 @@ def pmc(fetch_dir, write_dir):
     return dict(res)
 
 
+def sq(dirs):
+    acc = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(list)
+    for d in dirs:
+        for r in _rows(d, "*counter_collection.csv"):
+            acc[_short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for r in _rows(d, "*kernel_trace.csv"):
+            dur[_short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    out = {}
+    for k, v in acc.items():
+        o = {c: sum(x) / len(x) for c, x in v.items()}
+        if dur.get(k):
+            o["avg_us_in_pass"] = sum(dur[k]) / len(dur[k])
+            if "SQ_INSTS_VALU" in o:
+                o["valu_issue_frac"] = o["SQ_INSTS_VALU"] * 2 / (1024 * o["avg_us_in_pass"] * 1e-6 * 2.4e9)
+        out[k] = o
+    return out
+
+
 def main():
     mode = sys.argv[1]
     if mode == "trace":
@@ -73,6 +96,13 @@ def main():
                   + (f"{v['timed_avg_us']:>16.2f}" if last else ""))
         if "--out" in sys.argv:
             json.dump(t, open(sys.argv[sys.argv.index("--out") + 1], "w"), indent=1)
+    elif mode == "sq":
+        dirs = [a for a in sys.argv[2:] if not a.startswith("--") and a != (sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None)]
+        q = sq(dirs)
+        for k, v in q.items():
+            print(k, {c: (round(x, 3) if isinstance(x, float) and x < 100 else int(x)) for c, x in v.items()})
+        if "--out" in sys.argv:
+            json.dump(q, open(sys.argv[sys.argv.index("--out") + 1], "w"), indent=1)
     elif mode == "pmc":
         p = pmc(sys.argv[2], sys.argv[3])
         print(f"{'kernel':<28}{'FETCH KiB':>14}{'WRITE KiB':>14}{'HBM MB (corr)':>16}")
