@@ -298,6 +298,8 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
     a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = out->dL_dsh;
     a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
+    if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward: unknown accumulate bits 0x%x", out->accumulate);
+    a.accm = out->accumulate;
     char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, ScratchLayout(num_rendered).total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
     const ScratchLayout SL(num_rendered);

@@ -211,6 +211,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
 #endif
 }
 
+// Gradient output write: plain store, or (accumulate bit set, gsr_grads.accumulate) add into the
+// caller's existing gradient -- the same single fp32 add autograd's AccumulateGrad would do.
+__device__ inline void gput(float *p, size_t idx, float v, bool acc) { p[idx] = acc ? p[idx] + v : v; }
+
 // ------------------------------------------------------------------------------------------
 __device__ inline float3 dnormvdv(float3 v, float3 dv) {
     const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
@@ -225,7 +229,7 @@ __device__ inline float3 dnormvdv(float3 v, float3 dv) {
 // phase 2 writes the coefficient gradients, which depend only on the direction and dL/dRGB.
 template <typename ShPtr, typename OutPtr>
 __device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *campos, ShPtr sh,
-                                     const bool *clamped, float3 dL_dcolor, OutPtr dL_dsh) {
+                                     const bool *clamped, float3 dL_dcolor, OutPtr dL_dsh, bool acc = false) {
     const float3 d0 = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
     const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
     const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
@@ -286,11 +290,14 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *c
     for (int i = 0; i < 16; ++i) {
         if (i < M) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = i < active ? basis[i] * dRGB[c] : 0.f;
+            for (int c = 0; c < 3; ++c) {
+                const float v = i < active ? basis[i] * dRGB[c] : 0.f;
+                dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] + v : v;
+            }
         }
     }
     for (int i = 16; i < M; ++i)
-        for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = 0.f;
+        for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] : 0.f;
     const float3 dL_ddir = make_float3(dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2],
                                        dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
                                        dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]);
@@ -344,28 +351,33 @@ __device__ inline void gauss_bwd_one(
     const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec) {
-    // dL_dcolors / dL_dcov3D / dL_dscales / dL_drot may be NULL (gradient not requested)
-    if (!(radii[i] > 0)) {
+    float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec, int accm) {
+    // dL_dcolors / dL_dcov3D / dL_dscales / dL_drot may be NULL (gradient not requested); accm:
+    // gsr_grad_bits of the outputs to add into instead of overwrite
+    const bool a2 = accm & GSR_GRAD_MEANS2D, ac = accm & GSR_GRAD_COLORS, ao = accm & GSR_GRAD_OPACITY,
+               a3 = accm & GSR_GRAD_MEANS3D, acv = accm & GSR_GRAD_COV3D, ash = accm & GSR_GRAD_SH,
+               asc = accm & GSR_GRAD_SCALES, ar = accm & GSR_GRAD_ROTATIONS;
+    if (!(radii[i] > 0)) {  // zero gradient: accumulated outputs keep their content
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            dL_dmeans2D[3 * i + k] = 0.f; dL_dmeans3D[3 * i + k] = 0.f;
-            if (dL_dcolors) dL_dcolors[3 * i + k] = 0.f;
-            if (dL_dscales) dL_dscales[3 * i + k] = 0.f;
+            if (!a2) dL_dmeans2D[3 * i + k] = 0.f;
+            if (!a3) dL_dmeans3D[3 * i + k] = 0.f;
+            if (dL_dcolors && !ac) dL_dcolors[3 * i + k] = 0.f;
+            if (dL_dscales && !asc) dL_dscales[3 * i + k] = 0.f;
         }
-        dL_dopacity[i] = 0.f;
-        if (dL_dcov3D) {
+        if (!ao) dL_dopacity[i] = 0.f;
+        if (dL_dcov3D && !acv) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = 0.f;
         }
-        if (dL_drot) {
+        if (dL_drot && !ar) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) dL_drot[4 * i + k] = 0.f;
         }
         if (MC > 0) {
 #pragma unroll
             for (int k = 0; k < 3 * MC; ++k) s_row[k] = 0.f;
-        } else if (dL_dsh) {
+        } else if (dL_dsh && !ash) {
             for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
         }
         return;
@@ -380,15 +392,15 @@ __device__ inline void gauss_bwd_one(
         acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
         acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc.x;
     }
-    dL_dmeans2D[3 * i] = acc[0]; dL_dmeans2D[3 * i + 1] = acc[1]; dL_dmeans2D[3 * i + 2] = 0.f;
+    gput(dL_dmeans2D, 3 * i, acc[0], a2); gput(dL_dmeans2D, 3 * i + 1, acc[1], a2); gput(dL_dmeans2D, 3 * i + 2, 0.f, a2);
     // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
     if (act & GSR_ACT_SIGMOID_OPACITY) {
         const float o = rec[(size_t)kRecF4 * i + 1].y;
-        dL_dopacity[i] = acc[5] * ((1.f - o) * o);
+        gput(dL_dopacity, i, acc[5] * ((1.f - o) * o), ao);
     } else {
-        dL_dopacity[i] = acc[5];
+        gput(dL_dopacity, i, acc[5], ao);
     }
-    if (dL_dcolors) { dL_dcolors[3 * i] = acc[6]; dL_dcolors[3 * i + 1] = acc[7]; dL_dcolors[3 * i + 2] = acc[8]; }
+    if (dL_dcolors) { gput(dL_dcolors, 3 * i, acc[6], ac); gput(dL_dcolors, 3 * i + 1, acc[7], ac); gput(dL_dcolors, 3 * i + 2, acc[8], ac); }
     const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
 
     float vm[16], pj[16];
@@ -448,7 +460,7 @@ __device__ inline void gauss_bwd_one(
     }
     if (dL_dcov3D) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = dcov[k];
+        for (int k = 0; k < 6; ++k) gput(dL_dcov3D, 6 * i + k, dcov[k], acv);
     }
 #define VV(cc, rr) GM(V, cc, rr)
     const float dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
@@ -498,22 +510,22 @@ __device__ inline void gauss_bwd_one(
         bool cl[3];
         (void)sh_to_rgb(D, mean, campos, sh, cl);
         const float3 d = sh_backward(D, M, mean, campos, sh, cl, make_float3(acc[6], acc[7], acc[8]),
-                                     dL_dsh + (size_t)i * M * 3);
+                                     dL_dsh + (size_t)i * M * 3, ash);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
     } else if (dL_dsh) {
-        for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
+        if (!ash) for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
     }
-    dL_dmeans3D[3 * i] = dm0; dL_dmeans3D[3 * i + 1] = dm1; dL_dmeans3D[3 * i + 2] = dm2;
+    gput(dL_dmeans3D, 3 * i, dm0, a3); gput(dL_dmeans3D, 3 * i + 1, dm1, a3); gput(dL_dmeans3D, 3 * i + 2, dm2, a3);
     if (scales && !cov3D_precomp) {
         float3 ds; float4 dr;
         cov3d_backward(s3, scale_modifier, q, dcov, ds, dr);
         if (act & GSR_ACT_EXP_SCALES) { ds.x *= s3.x; ds.y *= s3.y; ds.z *= s3.z; }
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) dr = act_normalize_bwd(q, qn, dr);
-        if (dL_dscales) { dL_dscales[3 * i] = ds.x; dL_dscales[3 * i + 1] = ds.y; dL_dscales[3 * i + 2] = ds.z; }
-        if (dL_drot) { dL_drot[4 * i] = dr.x; dL_drot[4 * i + 1] = dr.y; dL_drot[4 * i + 2] = dr.z; dL_drot[4 * i + 3] = dr.w; }
+        if (dL_dscales) { gput(dL_dscales, 3 * i, ds.x, asc); gput(dL_dscales, 3 * i + 1, ds.y, asc); gput(dL_dscales, 3 * i + 2, ds.z, asc); }
+        if (dL_drot) { gput(dL_drot, 4 * i, dr.x, ar); gput(dL_drot, 4 * i + 1, dr.y, ar); gput(dL_drot, 4 * i + 2, dr.z, ar); gput(dL_drot, 4 * i + 3, dr.w, ar); }
     } else {
-        if (dL_dscales) { dL_dscales[3 * i] = 0.f; dL_dscales[3 * i + 1] = 0.f; dL_dscales[3 * i + 2] = 0.f; }
-        if (dL_drot) { dL_drot[4 * i] = 0.f; dL_drot[4 * i + 1] = 0.f; dL_drot[4 * i + 2] = 0.f; dL_drot[4 * i + 3] = 0.f; }
+        if (dL_dscales && !asc) { dL_dscales[3 * i] = 0.f; dL_dscales[3 * i + 1] = 0.f; dL_dscales[3 * i + 2] = 0.f; }
+        if (dL_drot && !ar) { dL_drot[4 * i] = 0.f; dL_drot[4 * i + 1] = 0.f; dL_drot[4 * i + 2] = 0.f; dL_drot[4 * i + 3] = 0.f; }
     }
 }
 
@@ -528,7 +540,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drot, int act, const float4 *__restrict__ rec) {
+    float *__restrict__ dL_drot, int act, const float4 *__restrict__ rec, int accm) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
@@ -542,10 +554,11 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
                                  scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos,
                                  radii, goff, part, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
-                                 act, rec);
+                                 act, rec, accm);
     if constexpr (MC > 0) {  // coalesced store of the dL/dSH rows
         __syncthreads();
-        sh_rows_from_lds<MC>(s_sh, nrow, dL_dsh + (size_t)i0 * RL);
+        if (accm & GSR_GRAD_SH) sh_rows_from_lds<MC, true>(s_sh, nrow, dL_dsh + (size_t)i0 * RL);
+        else sh_rows_from_lds<MC, false>(s_sh, nrow, dL_dsh + (size_t)i0 * RL);
     }
 }
 
@@ -568,7 +581,7 @@ static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
         a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
         a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
         a.radii, a.goff, a.part, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
-        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot, a.act, a.rec);
+        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot, a.act, a.rec, a.accm);
 }
 
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {

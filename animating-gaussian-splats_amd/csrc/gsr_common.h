@@ -163,8 +163,9 @@ __device__ inline void sh_rows_to_lds(const float *__restrict__ src, int nrow, f
     }
 }
 
-// The reverse copy (LDS rows -> contiguous global rows), float4 stores when aligned.
-template <int MC>
+// The reverse copy (LDS rows -> contiguous global rows), float4 stores when aligned; ACC adds the
+// rows to what dst holds (gradient accumulation).
+template <int MC, bool ACC = false>
 __device__ inline void sh_rows_from_lds(const float *s, int nrow, float *__restrict__ dst) {
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int n = nrow * RL;
@@ -178,16 +179,23 @@ __device__ inline void sh_rows_from_lds(const float *s, int nrow, float *__restr
                 const int e = 4 * q + j, r = e / RL;
                 f[j] = s[r * RS + (e - r * RL)];
             }
-            d4[q] = make_float4(f[0], f[1], f[2], f[3]);
+            float4 v = make_float4(f[0], f[1], f[2], f[3]);
+            if (ACC) {
+                const float4 o = d4[q];
+                v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+            }
+            d4[q] = v;
         }
         for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += kShBlock) {
             const int r = e / RL;
-            dst[e] = s[r * RS + (e - r * RL)];
+            const float v = s[r * RS + (e - r * RL)];
+            dst[e] = ACC ? dst[e] + v : v;
         }
     } else {
         for (int e = threadIdx.x; e < n; e += kShBlock) {
             const int r = e / RL;
-            dst[e] = s[r * RS + (e - r * RL)];
+            const float v = s[r * RS + (e - r * RL)];
+            dst[e] = ACC ? dst[e] + v : v;
         }
     }
 }

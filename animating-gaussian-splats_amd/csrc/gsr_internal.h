@@ -45,6 +45,7 @@ struct BwdArgs {
     // outputs
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
         *dL_drot;
+    int accm;  // gsr_grad_bits: outputs accumulated into instead of overwritten
 };
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);

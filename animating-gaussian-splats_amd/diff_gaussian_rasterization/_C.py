@@ -55,7 +55,7 @@ class _Gaussians(ctypes.Structure):
 class _Grads(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in (
         "dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
-        "dL_dscales", "dL_drotations")]
+        "dL_dscales", "dL_drotations")] + [("accumulate", ctypes.c_int)]
 
 
 _ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
@@ -110,7 +110,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 5  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 6  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -213,10 +213,13 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
-                                 activations=0, skip_unused=False):
+                                 activations=0, skip_unused=False, accumulate_into=None):
     """Returns the 8 gradients of the upstream binding.  ``skip_unused``: gradients of inputs that
     were not given (colours under SH, cov3D under scales/rotations and vice versa) come back as
-    empty tensors and their HBM writes are skipped."""
+    empty tensors and their HBM writes are skipped.  ``accumulate_into``: optional sequence of 8
+    tensors (or None) in output order; a given tensor (contiguous fp32 of the output's shape) receives
+    ``tensor + gradient`` in place (the kernel's single add = autograd's accumulation) and is
+    returned in that slot."""
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
@@ -229,13 +232,23 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     keep_col = not skip_unused or has(colors)
     keep_cov = not skip_unused or has(cov3D_precomp)
     keep_sr = not skip_unused or (has(scales) and has(rotations))
-    out = (e(P, 3), e(P, 3) if keep_col else e(0), e(P, 1), e(P, 3), e(P, 6) if keep_cov else e(0),
-           e(P, M, 3), e(P, 3) if keep_sr else e(0), e(P, 4) if keep_sr else e(0))
+    out = [e(P, 3), e(P, 3) if keep_col else e(0), e(P, 1), e(P, 3), e(P, 6) if keep_cov else e(0),
+           e(P, M, 3), e(P, 3) if keep_sr else e(0), e(P, 4) if keep_sr else e(0)]
+    acc_bits = 0
+    for k, t in enumerate(accumulate_into or ()):
+        if t is None or out[k].numel() == 0:
+            continue
+        if t.shape != out[k].shape or t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+            raise RuntimeError(f"accumulate_into[{k}]: expected a contiguous float32 {tuple(out[k].shape)} "
+                               f"tensor on {dev}")
+        out[k] = t
+        acc_bits |= 1 << k
+    out = tuple(out)
     if P == 0:
         return out
     dpix = dL_dout_color.contiguous().float()
     keep.append(dpix)
-    grads = _Grads(*[t.data_ptr() if t.numel() else None for t in out])
+    grads = _Grads(*[t.data_ptr() if t.numel() else None for t in out], acc_bits)
     alloc = _Allocator(dev)
     _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
                           geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),

@@ -38,6 +38,21 @@ class GaussianRasterizationSettings(NamedTuple):
     debug: bool = False
 
 
+def _accumulation_target(t):
+    """The leaf's existing ``.grad`` when the backward kernel may add into it in place (and the
+    Function then returns None for it): a leaf requiring grad whose gradient is a contiguous fp32
+    tensor of its shape, with no hooks that autograd's accumulation would have run.  Gives the same
+    value as autograd's AccumulateGrad (one fp32 add) without its separate read-read-write pass."""
+    if t is None or not isinstance(t, torch.Tensor) or t.numel() == 0 or not t.is_leaf or not t.requires_grad:
+        return None
+    g = t.grad
+    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != t.shape or g.requires_grad:
+        return None
+    if t._backward_hooks or getattr(t, "_post_accumulate_grad_hooks", None):
+        return None
+    return g
+
+
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales,
@@ -56,6 +71,8 @@ class _RasterizeGaussians(torch.autograd.Function):
             _C.rasterize_gaussians(*args)
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
+        # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
+        ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
@@ -72,8 +89,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                 sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
+        acc = [_accumulation_target(t) if need else None
+               for t, need in zip(ctx.leaves, (ctx.needs_input_grad[1], ctx.needs_input_grad[3],
+                                               ctx.needs_input_grad[4], ctx.needs_input_grad[0],
+                                               ctx.needs_input_grad[7], ctx.needs_input_grad[2],
+                                               ctx.needs_input_grad[5], ctx.needs_input_grad[6]))]
+        g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc))
+        for k, t in enumerate(acc):
+            if t is not None:
+                g[k] = None  # already accumulated into the leaf's .grad
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp,
-         grad_sh, grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(*args, skip_unused=True)
+         grad_sh, grad_scales, grad_rotations) = g
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities,
                 grad_scales, grad_rotations, grad_cov3Ds_precomp, None)
 
@@ -148,6 +174,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.opacity_shape = opacity_logits.shape
+        ctx.leaves = (means2D, colors, opacity_logits, means, None, sh, log_scales, quaternions)
         ctx.save_for_backward(colors, means, log_scales, quaternions, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
@@ -162,13 +189,20 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         colors, means, log_scales, quaternions, radii, sh, geomBuffer, binningBuffer, imgBuffer = \
             ctx.saved_tensors
         empty = torch.empty(0, device=means.device)
+        need = ctx.needs_input_grad
+        acc = [_accumulation_target(t) if n else None
+               for t, n in zip(ctx.leaves, (need[1], need[3], need[4], need[0], False, need[2], need[5], need[6]))]
+        if acc[2] is not None and acc[2].shape != (means.shape[0], 1):
+            acc[2] = None
         (g_means2D, g_colors, g_opacity, g_means, _g_cov3D, g_sh, g_scales, g_rot) = \
             _C.rasterize_gaussians_backward(
                 rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
                 rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                activations=_C.ACT_ALL, skip_unused=True)
-        need = ctx.needs_input_grad
-        return (g_means, g_means2D if need[1] else None, g_sh if sh.numel() else None,
-                g_colors if colors.numel() else None, g_opacity.view(ctx.opacity_shape), g_scales, g_rot,
-                None)
+                activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc)
+        done = [t is not None for t in acc]  # accumulated into the leaf's .grad: return None
+        return (None if done[3] else g_means, None if (done[0] or not need[1]) else g_means2D,
+                None if (done[5] or not sh.numel()) else g_sh,
+                None if (done[1] or not colors.numel()) else g_colors,
+                None if done[2] else g_opacity.view(ctx.opacity_shape),
+                None if done[6] else g_scales, None if done[7] else g_rot, None)

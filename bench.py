@@ -4,7 +4,8 @@ Metric: Msplats/s = P x views / wall-time(forward + backward) / 1e6, P counted p
 (SURVEY.md 8(d)).  Workload (BASELINE.json configs[2], the 1-GPU config the metric is quoted on):
 1M synthetic Gaussians, SH degree 3, 1920x1080, f = 1600, views from the 27-camera rig of
 configs[3] (heights {-0.8, 0, 0.8} x yaws {0, 40, ..., 320}).  One step = every rank renders
-``--views-per-rank`` views through the drop-in ``GaussianRasterizer`` on the render arguments of
+``--views-per-rank`` views (default 5: train.py:757 optimises on the summed losses of 5 views per
+step) through the drop-in ``GaussianRasterizer`` on the render arguments of
 shared.py:29-42 (activated once, before timing, and held as leaf tensors: SURVEY.md 8(d) times the
 rasterizer's forward + backward), backpropagates a fixed upstream dL/dcolor into them (gradients
 accumulate over the rank's views, as train.py sums view losses), and for N > 1 all-reduces (SUM)
@@ -288,8 +289,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--views-per-rank", type=int, default=1)
+    ap.add_argument("--views-per-rank", type=int, default=5,
+                    help="views rendered per GPU per step (train.py:757 sums the losses of 5 views "
+                         "per optimisation step)")
     ap.add_argument("--config", default="C3")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse the multi-rank path on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--call-site-steps", type=int, default=10,
                     help="steps timed for each train.py call-site variant (0 = skip)")
@@ -308,10 +314,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several gloo ranks on one GPU
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     _C.load_library()
@@ -333,7 +343,9 @@ def main():
     if cfg.sh_degree >= 0:
         act.pop("colors_precomp")
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
-    reducer = splat_dp.GradAllReduce([v for k, v in leaves.items() if k != "means2D"]) \
+    # N > 1: the gradients live in one flat bucket that backward accumulates into and RCCL reduces
+    # in place (no pack / unpack copies)
+    reducer = splat_dp.GradAllReduce([v for k, v in leaves.items() if k != "means2D"]).attach() \
         if dist is not None else None
 
     def views_of(it):
@@ -346,9 +358,12 @@ def main():
             img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
             img.backward(dl)
         if reducer is not None:
-            reducer()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
-        for p in leaves.values():
-            p.grad = None
+            reducer.reduce()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
+            reducer.zero_()
+            leaves["means2D"].grad = None
+        else:
+            for p in leaves.values():
+                p.grad = None
 
     def step_reference_call_site(it):  # train.py: create_render_arguments + Renderer + backward
         for ci in views_of(it):

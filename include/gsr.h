@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 5
+#define GSR_ABI_VERSION 6
 
 enum gsr_status {
     GSR_OK = 0,
@@ -95,11 +95,20 @@ typedef struct gsr_gaussians {
     int activations;             /* gsr_activation bit mask (ABI >= 2); 0 = activated inputs */
 } gsr_gaussians;
 
+/* Bits of gsr_grads.accumulate (ABI >= 6), one per output array. */
+enum gsr_grad_bits {
+    GSR_GRAD_MEANS2D = 1, GSR_GRAD_COLORS = 2, GSR_GRAD_OPACITY = 4, GSR_GRAD_MEANS3D = 8,
+    GSR_GRAD_COV3D = 16, GSR_GRAD_SH = 32, GSR_GRAD_SCALES = 64, GSR_GRAD_ROTATIONS = 128
+};
+
 /* Gradient outputs of gsr_backward, in the order _C.rasterize_gaussians_backward returns them.
  * Every element of every non-NULL array is written (no pre-zeroing needed).  dL_dmeans2D,
  * dL_dopacity, dL_dmeans3D (and dL_dsh when shs are given) are required; dL_dcolors, dL_dcov3D,
  * dL_dscales and dL_drotations may be NULL when the caller does not need them (e.g. dL_dcolors
- * under SH colour, dL_dcov3D when scales/rotations are given): their HBM writes are skipped. */
+ * under SH colour, dL_dcov3D when scales/rotations are given): their HBM writes are skipped.
+ * `accumulate` (gsr_grad_bits): the marked arrays already hold a gradient and receive
+ * old + new (one fp32 add, what torch's AccumulateGrad computes) instead of new -- gradient
+ * accumulation over the views of a step without a separate add pass. */
 typedef struct gsr_grads {
     float *dL_dmeans2D;   /* (P,3)  NDC units, z = 0 */
     float *dL_dcolors;    /* (P,3) */
@@ -109,6 +118,7 @@ typedef struct gsr_grads {
     float *dL_dsh;        /* (P,M,3) or NULL when M == 0 */
     float *dL_dscales;    /* (P,3) */
     float *dL_drotations; /* (P,4) */
+    int accumulate;       /* gsr_grad_bits (ABI >= 6); 0 = overwrite every output */
 } gsr_grads;
 
 /* Forward: preprocess -> tile binning -> per-tile depth sort -> alpha blend (colour + depth).

@@ -33,6 +33,18 @@ def _worker(rank, world, port, q):
         splat_dp.GradAllReduce(params)()
         out["grads"] = [p.grad.numpy() for p in params]
         out["local"] = [x.numpy() for x in local]
+        # 1b) in-place bucket: backward accumulates into the attached bucket, reduce sums over ranks
+        ps = [torch.nn.Parameter(torch.ones(7, 3)), torch.nn.Parameter(torch.ones(5, 4))]
+        red = splat_dp.GradAllReduce(ps).attach()
+        ws = [torch.randn(p.shape, generator=g) for p in ps]
+        for _ in range(2):  # two views accumulate
+            sum((p * w).sum() for p, w in zip(ps, ws)).backward()
+        red.reduce()
+        out["inplace"] = [p.grad.clone().numpy() for p in ps]
+        out["inplace_local"] = [(2 * w).numpy() for w in ws]
+        assert all(p.grad.data_ptr() >= red.flat.data_ptr() for p in ps)  # still views of the bucket
+        red.zero_()
+        out["inplace_zeroed"] = float(sum(p.grad.abs().sum() for p in ps))
         # 2) densify statistics: views sharded round-robin, then SUM/SUM/MAX
         radii, grads = GOLD["dstat_in_radii"], GOLD["dstat_in_grad"]
         st = splat_dp.DensifyStats(radii.shape[1], "cpu")
@@ -62,6 +74,9 @@ def test_dp_allreduce_and_densify_stats_world2():
     for r in range(world):
         for a, b0, b1 in zip(res[r]["grads"], res[0]["local"], res[1]["local"]):
             np.testing.assert_allclose(a, b0 + b1, rtol=1e-6, atol=1e-6)
+        for a, b0, b1 in zip(res[r]["inplace"], res[0]["inplace_local"], res[1]["inplace_local"]):
+            np.testing.assert_allclose(a, b0 + b1, rtol=1e-6, atol=1e-6)
+        assert res[r]["inplace_zeroed"] == 0.0
         # sharded accumulation + all-reduce == the reference's sequential accumulation
         np.testing.assert_array_equal(res[r]["vis"], GOLD["dstat_out_visibility_count"])
         np.testing.assert_array_equal(res[r]["maxr"], GOLD["dstat_out_max_radii"])
