@@ -24,6 +24,18 @@ __global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *
                                                          uint32_t *__restrict__ tile_order) {
     __shared__ uint32_t s_red[16];
     __shared__ uint32_t s_hist[kOrderBuckets];
+    if (T <= kScanRegs * (int)blockDim.x) {  // costs prefetched into registers, all loads in flight
+        const int c = div_up(T, (int)blockDim.x), t0 = threadIdx.x * c;
+        uint32_t cost[kScanRegs];
+#pragma unroll
+        for (int i = 0; i < kScanRegs; ++i) {
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (i < c && t0 + i < T) q = reinterpret_cast<const uint4 *>(tile_cost)[t0 + i];
+            cost[i] = q.x + q.y + q.z + q.w;
+        }
+        lpt_order_regs<kScanRegs>(T, c, cost, tile_order, s_hist, s_red);
+        return;
+    }
     lpt_order(T, [&](int t) {
         const uint4 c = reinterpret_cast<const uint4 *>(tile_cost)[t];
         return c.x + c.y + c.z + c.w;

@@ -480,6 +480,48 @@ __device__ inline void lpt_order(int T, CostFn cost, uint32_t *__restrict__ orde
         order[atomicAdd(&s_hist[kOrderBuckets - 1 - (cost(t) >> shift)], 1u)] = (uint32_t)t;
 }
 
+// The same LPT order when every thread already holds the costs of the c consecutive tiles
+// t = threadIdx.x * c + i (i < c <= C) in registers: the single-block scan kernels prefetch them with
+// every load in flight instead of re-reading global memory in dependent strided loops.
+template <int C>
+__device__ inline void lpt_order_regs(int T, int c, const uint32_t (&cost)[C], uint32_t *__restrict__ order,
+                                      uint32_t *s_hist, uint32_t *s_red) {
+    const int t0 = threadIdx.x * c;
+    uint32_t mx = 0;
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+        if (i < c && t0 + i < T) mx = max(mx, cost[i]);
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = mx;
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
+    __syncthreads();
+    mx = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mx = max(mx, s_red[w]);
+    int shift = 0;
+    while ((mx >> shift) >= (uint32_t)kOrderBuckets) ++shift;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+        if (i < c && t0 + i < T) atomicAdd(&s_hist[kOrderBuckets - 1 - (cost[i] >> shift)], 1u);
+    __syncthreads();
+    uint32_t carry = 0;
+    for (int base = 0; base < kOrderBuckets; base += blockDim.x) {
+        const int b = base + threadIdx.x;
+        const uint32_t h = b < kOrderBuckets ? s_hist[b] : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32(h, s_red, &tot) + carry;
+        if (b < kOrderBuckets) s_hist[b] = ex;
+        carry += tot;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+        if (i < c && t0 + i < T)
+            order[atomicAdd(&s_hist[kOrderBuckets - 1 - (cost[i] >> shift)], 1u)] = (uint32_t)(t0 + i);
+}
+// Tiles per thread held in registers by the single-block kernels (1024 threads): T <= 16384.
+constexpr int kScanRegs = 16;
+
 // XCD-aware bijection over T tiles: blocks b, b+8, ... (one XCD under round-robin dispatch) take a
 // contiguous run of tiles, so neighbouring tiles share Gaussian records in one L2.  Speed only.
 __device__ inline int remap_tile(int b, int T) {

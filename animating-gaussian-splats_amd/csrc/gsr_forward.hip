@@ -147,7 +147,10 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
 
 // ------------------------------------------------------------------------------------------
 // Single block (1024 threads): exclusive scan of the T tile counts -> ranges/cursors, and of the
-// NB chunk sums -> chunk emission offsets.  meta[0] = K.
+// NB chunk sums -> chunk emission offsets.  meta[0] = K.  Up to 16384 tiles every thread holds its
+// (at most 16) consecutive counts in registers, loaded with every load in flight, so the kernel does
+// one block scan instead of a chain of dependent strided load-scan rounds; larger grids take the
+// strided path.
 __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t *__restrict__ tile_count,
                                                    uint2 *__restrict__ ranges,
                                                    uint32_t *__restrict__ tile_cursor,
@@ -161,6 +164,42 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
     __shared__ uint32_t s_hist[kOrderBuckets];
     __shared__ uint32_t s_cls[3];
     if (threadIdx.x < 3) s_cls[threadIdx.x] = 0;
+    if (T <= kScanRegs * (int)blockDim.x && NB <= (int)blockDim.x) {
+        // fast path: thread owns tiles [tid c, tid c + c); all counts loaded up front, one block scan
+        const int c = div_up(T, (int)blockDim.x), t0 = threadIdx.x * c;
+        uint32_t cnt[kScanRegs];
+#pragma unroll
+        for (int i = 0; i < kScanRegs; ++i) cnt[i] = (i < c && t0 + i < T) ? tile_count[t0 + i] : 0u;
+        const uint32_t bsum = (int)threadIdx.x < NB ? block_sums[threadIdx.x] : 0u;
+        uint32_t mine = 0;
+#pragma unroll
+        for (int i = 0; i < kScanRegs; ++i) mine += cnt[i];
+        uint32_t K;
+        uint32_t ex = block_excl_scan_u32(mine, s_red, &K);
+#pragma unroll
+        for (int i = 0; i < kScanRegs; ++i) {
+            const int t = t0 + i;
+            if (i < c && t < T) {
+                ranges[t] = cnt[i] ? make_uint2(ex, ex + cnt[i]) : make_uint2(0, 0);  // empty: {0,0} like the reference
+                tile_cursor[t] = ex;
+                if (cnt[i] > (uint32_t)kFwdSortCap) sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
+            }
+            ex += cnt[i];
+        }
+        uint32_t btot;
+        const uint32_t bex = block_excl_scan_u32(bsum, s_red, &btot);  // contains the barrier s_cls needs
+        if ((int)threadIdx.x < NB) block_off[threadIdx.x] = bex;
+        if (threadIdx.x == 0) {
+            meta[0] = K;
+            if (host_words) {
+                for (int q = 0; q < 3; ++q)
+                    __hip_atomic_store(host_words + 1 + q, s_cls[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(host_words, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        lpt_order_regs<kScanRegs>(T, c, cnt, tile_order, s_hist, s_red);
+        return;
+    }
     uint32_t carry = 0;
     for (int base = 0; base < T; base += blockDim.x) {
         const int t = base + threadIdx.x;
