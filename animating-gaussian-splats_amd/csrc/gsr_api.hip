@@ -543,6 +543,27 @@ int gsr_adam_step(int ntensors, const gsr_adam_tensor *tensors, double beta1, do
     return GSR_OK;
 }
 
+int gsr_views_pack(int frames, int H, int W, const uint8_t *rgb, const uint8_t *seg, float *images,
+                   float *seg_masks, void *stream) {
+    if (frames < 0 || H < 0 || W < 0) return fail(GSR_ERR_ARG, "views_pack: negative size");
+    if (frames == 0 || H == 0 || W == 0) return GSR_OK;
+    if ((long long)H * W > (1ll << 29)) return fail(GSR_ERR_UNSUPPORTED, "views_pack: frame of %d x %d too large", H, W);
+    if (frames > 65535) return fail(GSR_ERR_UNSUPPORTED, "views_pack: more than 65535 frames in one call");
+    if (!rgb || !images) return fail(GSR_ERR_ARG, "views_pack: null rgb / images");
+    if ((seg == nullptr) != (seg_masks == nullptr))
+        return fail(GSR_ERR_ARG, "views_pack: seg and seg_masks must be given together");
+    const int HW = H * W;
+    if (HW % 4 == 0) {  // the vector path's alignment contract
+        if (((uintptr_t)rgb & 3) || (seg && ((uintptr_t)seg & 3)) || ((uintptr_t)images & 15) ||
+            (seg_masks && ((uintptr_t)seg_masks & 15)))
+            return fail(GSR_ERR_ARG, "views_pack: rgb / seg must be 4-byte and outputs 16-byte aligned");
+    }
+    hipStream_t s = (hipStream_t)stream;
+    Phase ph(s, "views_pack");
+    HIP_TRY(launch_views_pack(frames, HW, rgb, seg, images, seg_masks, s));
+    return GSR_OK;
+}
+
 int gsr_profile_enable(int on) {
     std::lock_guard<std::mutex> lk(g_prof_mu);
     g_prof_on = on != 0;

@@ -110,4 +110,8 @@ struct AdamTable {
 int adam_blocks(long long n);
 hipError_t launch_adam(const AdamTable &tab, hipStream_t s);
 
+// camera frames -> view tensors (gsr_io.hip)
+hipError_t launch_views_pack(int frames, int HW, const uint8_t *rgb, const uint8_t *seg, float *img, float *msk,
+                             hipStream_t s);
+
 }  // namespace gsr

@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "gsr_profile_enable", "gsr_profile_select", "gsr_profile_reset", "gsr_profile_read", "gsr_buffer_offsets",
     "gsr_ssim_scratch_bytes", "gsr_l1_ssim_forward", "gsr_l1_ssim_backward",
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
-    "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step",
+    "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
 )
 
 
@@ -110,7 +110,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 6  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 7  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 

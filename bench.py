@@ -284,6 +284,88 @@ def densify_call_site(steps, cfg, cam, dev):
     return out
 
 
+def _reference_timestep_views(md, t, root, dev):
+    """shared.py:127-171's per-view formatting composed from the reference's own ops (PIL on one
+    thread, float on the host, one upload per tensor, permute / divide / stack on the GPU), for the
+    I/O leg's comparison only."""
+    import copy
+    from PIL import Image
+    out = []
+    for c, fn in enumerate(md["fn"][t]):
+        m = torch.tensor(np.array(copy.deepcopy(Image.open(os.path.join(root, "seg", fn.replace(".jpg", ".png"))))
+                                  ).astype(np.float32)).float().to(dev)
+        img = torch.tensor(np.array(copy.deepcopy(Image.open(os.path.join(root, "ims", fn))))).float().to(dev)
+        out.append((img.permute(2, 0, 1) / 255, torch.stack((m, torch.zeros_like(m), 1 - m))))
+    return out
+
+
+def io_call_site(timesteps, dev, W=640, H=360, C=27):
+    """Frames per second of the data path on a synthetic sequence in the
+    reference's layout (27 cameras of 640 x 360 -- the dataset's frame size -- JPEG + PNG):
+    splat_io.load_all_views (thread-pool decode into one pinned 8-bit batch, one upload, one
+    gsr_views_pack launch per timestep) vs the reference's per-view composition; plus the pack
+    kernel's device time and its GB/s over 4 B read + 24 B written per pixel."""
+    import shutil
+    import tempfile
+    import splat_io
+    import splat_scenes as S
+    from PIL import Image
+    from diff_gaussian_rasterization import _C
+    root = tempfile.mkdtemp(prefix="gsr_io_")
+    try:
+        rng = np.random.default_rng(0)
+        yy, xx = np.mgrid[0:H, 0:W]
+        md = {"w": W, "h": H, "fn": [], "k": [], "w2c": []}
+        K = S.intrinsics(0.8 * W, W, H).tolist()
+        for t in range(timesteps + 1):
+            md["fn"].append([]); md["k"].append([]); md["w2c"].append([])
+            for c in range(C):
+                fn = f"{c}/{t:06d}.jpg"
+                for sub in ("ims", "seg"):
+                    os.makedirs(os.path.join(root, sub, str(c)), exist_ok=True)
+                base = np.stack([xx * 255 // (W - 1), yy * 255 // (H - 1), (xx + yy + 9 * c + t) % 256], -1)
+                img = np.clip(base + rng.integers(-20, 21, size=(H, W, 3)), 0, 255).astype(np.uint8)
+                Image.fromarray(img).save(os.path.join(root, "ims", fn), quality=90)
+                inside = ((xx - W / 2) ** 2 + (yy - H / 2) ** 2) < (H / 3 + c) ** 2
+                Image.fromarray(inside.astype(np.uint8), mode="L").save(os.path.join(root, "seg", fn.replace(".jpg", ".png")))
+                md["fn"][t].append(fn); md["k"][t].append(K)
+                md["w2c"][t].append(S.look_at(360.0 * c / C, 0.2, 4.0).tolist())
+        frames = timesteps * C
+        splat_io.load_all_views(md, 1, root, device=dev)  # warm: pool start, pinned allocator, kernel
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        views = splat_io.load_all_views(md, timesteps, root, device=dev)
+        torch.cuda.synchronize()
+        ours = time.perf_counter() - t0
+        _reference_timestep_views(md, 1, root, dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ref = [_reference_timestep_views(md, t, root, dev) for t in range(1, timesteps + 1)]
+        torch.cuda.synchronize()
+        refs = time.perf_counter() - t0
+        same = all(torch.equal(v.image, r[0]) and torch.equal(v.segmentation_mask, r[1])
+                   for vs, rs in zip(views, ref) for v, r in zip(vs, rs))
+        # device time of the pack kernel over one timestep already resident in HBM
+        rgb = torch.randint(0, 256, (C, H, W, 3), dtype=torch.uint8, device=dev)
+        seg = torch.randint(0, 2, (C, H, W), dtype=torch.uint8, device=dev)
+        splat_io.pack_views(rgb, seg)
+        _C.profile_reset(); _C.profile_select(["views_pack"]); _C.profile_enable(True)
+        for _ in range(20):
+            splat_io.pack_views(rgb, seg)
+        _C.profile_enable(False)
+        tot, n = _C.profile_read("views_pack")
+        _C.profile_select(None)
+        kms = tot / max(n, 1)
+        return {"frames": frames, "frame": f"{W}x{H}", "cameras": C, "timesteps": timesteps,
+                "workers": splat_io.TimestepDecoder().workers,
+                "native_frames_per_s": round(frames / ours, 1), "reference_frames_per_s": round(frames / refs, 1),
+                "bitwise_equal_to_reference_ops": bool(same),
+                "pack_kernel_ms_per_timestep": round(kms, 5),
+                "pack_GBps": round(28 * C * H * W / (kms * 1e-3) / 1e9, 1)}
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -303,6 +385,9 @@ def main():
                     help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip)")
     ap.add_argument("--densify-steps", type=int, default=5,
                     help="densify.py iterations timed per variant at the bench resolution (0 = skip)")
+    ap.add_argument("--io-timesteps", type=int, default=2,
+                    help="timesteps of 27 synthetic 640x360 frames loaded per variant by the data-path "
+                         "leg (0 = skip)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="untimed steps with events on every phase (per-kernel breakdown)")
     args = ap.parse_args()
@@ -441,6 +526,7 @@ def main():
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
     loss_site = loss_call_site(args.loss_steps, cams[0], leaves, dev) if args.loss_steps > 0 else None
     dens_site = densify_call_site(args.densify_steps, cfg, cams[0], dev) if args.densify_steps > 0 else None
+    io_site = io_call_site(args.io_timesteps, dev) if args.io_timesteps > 0 and rank == 0 else None
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
     import splat_dp
     used = sorted({ci for it in range(args.warmup + args.probe_steps, args.warmup + args.probe_steps + args.steps)
@@ -519,6 +605,7 @@ def main():
             "call_site": call_site,
             "loss_call_site": loss_site,
             "densify_call_site": dens_site,
+            "io_call_site": io_site,
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

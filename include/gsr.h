@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 6
+#define GSR_ABI_VERSION 7
 
 enum gsr_status {
     GSR_OK = 0,
@@ -254,9 +254,18 @@ typedef struct gsr_adam_tensor {
 int gsr_adam_step(int ntensors, const gsr_adam_tensor *tensors, double beta1, double beta2, double eps,
                   void *stream);
 
+/* ---- Camera frames of one timestep -> the reference's view tensors (ABI >= 7) ----
+ * Replaces the per-view tensor formatting of load_timestep_views (shared.py:127-171) for `frames`
+ * frames of H x W pixels at once.  Inputs are device pointers to the decoded 8-bit data: `rgb`
+ * (frames, H, W, 3) interleaved, `seg` (frames, H, W) or NULL.  Outputs (contiguous fp32):
+ * `images` (frames, 3, H, W) = rgb / 255 (as torch computes it on the GPU: x * (1.0f / 255.0f)),
+ * `seg_masks` (frames, 3, H, W) = (m, 0, 1 - m) with m = float(seg), or NULL when seg is NULL. */
+int gsr_views_pack(int frames, int H, int W, const uint8_t *rgb, const uint8_t *seg, float *images,
+                   float *seg_masks, void *stream);
+
 /* Per-phase device timing with HIP events recorded on the call's stream (off by default).
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
- * "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam".  gsr_profile_read synchronises on the recorded events. */
+ * "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam", "views_pack".  gsr_profile_read synchronises on the recorded events. */
 int gsr_profile_enable(int on);
 /* Restrict event recording to a comma-separated list of phases (NULL or "" = every phase), so a
  * timed region can carry the events of one kernel only.  Host-side timers are unaffected. */

@@ -1,8 +1,9 @@
 """Generate golden vectors by running the REFERENCE's own Python callers of the rasterizer.
 
 Run in the build container only (needs /root/reference, which does not exist on the GPU box):
-    python tests/golden/gen_golden.py
-Writes tests/golden/reference_harness.npz (data only: inputs and the reference's outputs).
+    python tests/golden/gen_golden.py          (both files)   |   python tests/golden/gen_golden.py --io
+Writes tests/golden/reference_harness.npz and reference_io.npz (data only: inputs and the
+reference's outputs; the I/O fixtures hold the small image / .pth files the reference read).
 
 What is captured:
   * create_render_settings (shared.py:64-124) for the benchmark/test cameras and the inference rig
@@ -212,5 +213,101 @@ def main():
     print(f"wrote {len(out)} arrays to tests/golden/reference_harness.npz")
 
 
+def _write_sequence(root, W, H, T, C, seed):
+    """A tiny camera sequence in the reference's dataset layout (train_meta.json + ims/*.jpg +
+    seg/*.png), written with PIL from seeded arrays; returns the metadata dict."""
+    import json
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    os.makedirs(os.path.join(root, "ims"), exist_ok=True)
+    os.makedirs(os.path.join(root, "seg"), exist_ok=True)
+    md = {"w": W, "h": H, "fn": [], "k": [], "w2c": []}
+    yy, xx = np.mgrid[0:H, 0:W]
+    for t in range(T):
+        md["fn"].append([]); md["k"].append([]); md["w2c"].append([])
+        for c in range(C):
+            fn = f"{c}/{t:06d}.jpg"
+            os.makedirs(os.path.join(root, "ims", str(c)), exist_ok=True)
+            os.makedirs(os.path.join(root, "seg", str(c)), exist_ok=True)
+            base = np.stack([xx * 255 // max(W - 1, 1), yy * 255 // max(H - 1, 1), (xx + yy + 40 * c) % 256], -1)
+            img = np.clip(base + rng.integers(-30, 31, size=(H, W, 3)), 0, 255).astype(np.uint8)
+            Image.fromarray(img).save(os.path.join(root, "ims", fn), quality=85)
+            inside = ((xx - W / 2 - 3 * t) ** 2 + (yy - H / 2 + c) ** 2) < (min(W, H) / 3) ** 2
+            seg_png = os.path.join(root, "seg", fn.replace(".jpg", ".png"))
+            if c % 2 == 0:
+                Image.fromarray(inside.astype(np.uint8), mode="L").save(seg_png)
+            else:  # 1-bit PNG: numpy reads it as bool
+                Image.fromarray(inside).convert("1").save(seg_png)
+            f = 0.8 * W + 10 * c
+            md["fn"][t].append(fn)
+            md["k"][t].append([[f, 0.0, W / 2 + c], [0.0, f, H / 2 - t], [0.0, 0.0, 1.0]])
+            md["w2c"][t].append(train.create_transformation_matrix(30.0 * c + 5 * t, 0.1 * t, 4.0).tolist())
+    with open(os.path.join(root, "train_meta.json"), "w") as fh:
+        json.dump(md, fh)
+    return md
+
+
+def main_io():
+    """Fixtures of the data / format row: the reference's load_timestep_views
+    (shared.py:127-171) on two tiny sequences written here (one with a pixel count that is not a
+    multiple of 4), and a parameter dict written by its export_parameters (densify.py:190-198) and
+    read back by load_densified_initial_parameters (train.py:155-163).  The image / mask files and
+    the .pth are stored as bytes (data), with the reference's outputs.  Writes reference_io.npz."""
+    global train
+    import json
+    import tempfile
+    from pathlib import Path
+    _install_shims()
+    sys.modules["wandb"].save = lambda *a, **k: None
+    sys.path.insert(0, REF)
+    shared = importlib.import_module("shared")
+    densify = importlib.import_module("densify")
+    train = importlib.import_module("train")
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, (W, H, T, C, seed) in {"a": (40, 24, 2, 3, 1), "b": (37, 23, 1, 2, 2)}.items():
+            root = os.path.join(tmp, name)
+            md = _write_sequence(root, W, H, T, C, seed)
+            out[f"io_{name}_meta"] = np.frombuffer(json.dumps(md).encode(), dtype=np.uint8)
+            for t in range(T):
+                for c, fn in enumerate(md["fn"][t]):
+                    for sub, f in (("ims", fn), ("seg", fn.replace(".jpg", ".png"))):
+                        with open(os.path.join(root, sub, f), "rb") as fh:
+                            out[f"io_{name}_file_{sub}_{t}_{c}"] = np.frombuffer(fh.read(), dtype=np.uint8)
+                views = shared.load_timestep_views(dataset_metadata=md, timestep=t, sequence_path=Path(root))
+                for v in views:
+                    c = v.camera_index
+                    out[f"io_{name}_t{t}_c{c}_image"] = v.image.contiguous().numpy()
+                    out[f"io_{name}_t{t}_c{c}_mask"] = v.segmentation_mask.contiguous().numpy()
+                    out[f"io_{name}_t{t}_c{c}_image_strides"] = np.array(v.image.stride())
+                    rs = v.render_settings
+                    out[f"io_{name}_t{t}_c{c}_viewmatrix"] = rs.viewmatrix.numpy()
+                    out[f"io_{name}_t{t}_c{c}_projmatrix"] = rs.projmatrix.numpy()
+                    out[f"io_{name}_t{t}_c{c}_campos"] = rs.campos.numpy()
+                    out[f"io_{name}_t{t}_c{c}_tanfov"] = np.array([rs.tanfovx, rs.tanfovy])
+        # .pth parameter dict: reference export -> bytes; reference load -> values
+        gd = torch.Generator().manual_seed(7)
+        params = {k: torch.nn.Parameter(torch.randn(*shp, generator=gd))
+                  for k, shp in (("means", (50, 3)), ("colors", (50, 3)), ("segmentation_masks", (50, 3)),
+                                 ("rotation_quaternions", (50, 4)), ("opacity_logits", (50, 1)),
+                                 ("log_scales", (50, 3)), ("camera_matrices", (4, 3)), ("camera_center", (4, 3)))}
+        seq = Path(tmp) / "seq"
+        seq.mkdir()
+        densify.export_parameters(sequence_path=seq, parameters=params)
+        with open(seq / "densified_initial_gaussian_cloud_parameters.pth", "rb") as fh:
+            out["io_pth_bytes"] = np.frombuffer(fh.read(), dtype=np.uint8)
+        loaded = train.load_densified_initial_parameters(Path(tmp), "seq")
+        out["io_pth_keys"] = np.frombuffer(json.dumps(list(loaded.keys())).encode(), dtype=np.uint8)
+        for k, v in loaded.items():
+            out[f"io_pth_val_{k}"] = v.detach().numpy()
+            out[f"io_pth_rg_{k}"] = np.array(bool(v.requires_grad))
+    np.savez_compressed(os.path.join(HERE, "reference_io.npz"), **out)
+    print(f"wrote {len(out)} arrays to tests/golden/reference_io.npz")
+
+
 if __name__ == "__main__":
-    main()
+    if "--io" in sys.argv[1:]:
+        main_io()
+    else:
+        main()
+        main_io()
