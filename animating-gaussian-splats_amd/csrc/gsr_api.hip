@@ -165,7 +165,7 @@ void carve_image(FwdArgs &a, char *base) {
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K);
-    a.keys = (uint64_t *)(base + L.keys); a.vals = (uint32_t *)(base + L.vals);
+    a.pairs = (uint4 *)(base + L.pairs);
     a.point_list = (uint32_t *)(base + L.point_list);
     a.slot_emit = (uint32_t *)(base + L.slot_emit);
 }
@@ -188,7 +188,7 @@ int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const BinningLayout b(K);
     const size_t v[12] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
                           im.ranges, im.final_T, im.n_contrib, im.tile_maxc,
-                          b.keys, b.point_list, b.slot_emit};
+                          b.pairs, b.point_list, b.slot_emit};
     int n = 0;
     for (; n < 12 && n < max_out; ++n) out[n] = v[n];
     return n;

@@ -18,6 +18,7 @@ constexpr int kTileH = 16;
 constexpr int kTilePix = kTileW * kTileH;  // 256 = 4 wave64 per tile block
 constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic abc, dopacity, dcolour rgb
 constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
+__host__ __device__ inline uint64_t pair_key(uint4 r) { return ((uint64_t)r.y << 32) | r.x; }
 constexpr int kFwdSortCap = 1024;  // lists up to this length are depth-sorted inside k_render_fwd
 // host-mapped words published by k_bin_scan: [0] = K (written last, release), [1] = number of
 // tiles longer than kFwdSortCap (sorted by k_tile_sort before the render), [2..3] unused
@@ -92,11 +93,13 @@ struct ImageLayout {
 // BINNING (per Gaussian-tile pair, K): sort keys + their emission index, sorted Gaussian list,
 // emission index of every sorted slot (where the backward stores the slot's gradient record).
 struct BinningLayout {
-    size_t keys, vals, point_list, slot_emit, total;
+    size_t pairs, point_list, slot_emit, total;
     __host__ __device__ BinningLayout(int K) {
         size_t o = 0;
-        keys = o;       o = align256(o + sizeof(uint64_t) * (K > 0 ? K : 1));
-        vals = o;       o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));  // emission index of each key
+        // one 16-byte record per pair: (index, depth bits, emission index, 0) -- the 64-bit sort key
+        // (depth_bits << 32 | index) in .x/.y and its payload in .z, so k_bin_emit's scatter is ONE
+        // store per pair (the scatter is bound by scattered line requests, not bytes)
+        pairs = o;      o = align256(o + sizeof(uint4) * (K > 0 ? K : 1));
         point_list = o; o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
         slot_emit = o;  o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));  // sorted slot -> emission
         total = o;

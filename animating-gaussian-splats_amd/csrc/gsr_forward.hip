@@ -4,8 +4,9 @@
 //   k_preprocess   1 thread / Gaussian: cull, Sigma3D, EWA Sigma2D, conic, radius, tile rect, SH->RGB
 //   k_bin_count    chunked over Gaussians: LDS tile histogram -> one global add per (chunk, tile)
 //   k_bin_scan     1 block: exclusive scan of tile counts -> tile ranges; scan of chunk sums; K
-//   k_bin_emit     chunked: re-count in LDS, reserve a (chunk, tile) slab, scatter 64-bit keys
-//                  (depth_bits << 32 | gaussian) into their tile's range; exclusive emission offsets
+//   k_bin_emit     chunked: re-count in LDS, reserve a (chunk, tile) slab, scatter one 16-byte
+//                  record per pair (64-bit key depth_bits << 32 | gaussian + emission index) into
+//                  its tile's range; exclusive emission offsets
 //   k_tile_sort    1 block / tile: sort the tile's keys by (depth bits, index) in LDS (bitonic),
 //                  write the Gaussian list + the emission->slot map used by the backward reduction
 //   k_render_fwd   1 block (4 wave64) / 16x16 tile: front-to-back blend of colour and depth
@@ -22,6 +23,14 @@ namespace gsr {
 
 #ifdef GSR_TRACE
 __device__ uint64_t *g_trace_fwd;
+__device__ uint64_t *g_trace_emit;  // per k_bin_emit block: start, counted, reserved, end
+#define GSR_EMIT_STAMP(k)                                                                        \
+    do {                                                                                         \
+        if (g_trace_emit && threadIdx.x == 0)                                                    \
+            g_trace_emit[4 * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime();               \
+    } while (0)
+#else
+#define GSR_EMIT_STAMP(k) do {} while (0)
 #endif
 
 // ------------------------------------------------------------------------------------------
@@ -255,12 +264,12 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
                                                   const uint32_t *__restrict__ block_off,
                                                   uint32_t *__restrict__ tile_cursor,
                                                   uint32_t *__restrict__ goff,
-                                                  uint64_t *__restrict__ keys,
-                                                  uint32_t *__restrict__ vals, uint32_t K) {
+                                                  uint4 *__restrict__ pairs, uint32_t K) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
     __shared__ uint32_t s_red[16];
     const int b = blockIdx.x;
     const int g0 = b * CH, g1 = min(P, g0 + CH);
+    GSR_EMIT_STAMP(0);
     if (USE_LDS) {
         for (int t = threadIdx.x; t < T; t += blockDim.x) s_cur[t] = 0;
         __syncthreads();
@@ -272,11 +281,13 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
                 for (int x = x0; x < x1; ++x) atomicAdd(&s_cur[y * gx + x], 1u);
         }
         __syncthreads();
+        GSR_EMIT_STAMP(1);
         for (int t = threadIdx.x; t < T; t += blockDim.x) {
             const uint32_t c = s_cur[t];
             s_cur[t] = c ? atomicAdd(&tile_cursor[t], c) : 0u;
         }
         __syncthreads();
+        GSR_EMIT_STAMP(2);
     }
     // emission offsets (exclusive scan of tiles over Gaussian index) + key scatter
     uint32_t carry = block_off[b];
@@ -291,34 +302,26 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
             if (n) {
                 const uint2 r = rects[g];
                 const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
-                const uint64_t key_lo = (uint64_t)(uint32_t)g;
-                const uint64_t key = ((uint64_t)__float_as_uint(depth[g]) << 32) | key_lo;
+                const uint32_t dbits = __float_as_uint(depth[g]);
                 uint32_t e = ex;  // emission index: y-major over the rect, as the reference emits
                 for (int y = y0; y < y1; ++y)
                     for (int x = x0; x < x1; ++x, ++e) {
                         const int t = y * gx + x;
                         const uint32_t pos = USE_LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_cursor[t], 1u);
-                        keys[pos] = key;
-                        vals[pos] = e;
+                        pairs[pos] = make_uint4((uint32_t)g, dbits, e, 0u);
                     }
             }
         }
     }
     if (b == gridDim.x - 1 && threadIdx.x == 0) goff[P] = K;
+#ifdef GSR_TRACE
+    __syncthreads();
+    GSR_EMIT_STAMP(3);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
 // Per-tile sort of (depth_bits << 32 | index) keys, then outputs.
-__device__ inline void tile_sort_write(uint64_t key, uint32_t slot, int tx, int ty,
-                                       const uint2 *__restrict__ rects,
-                                       const uint32_t *__restrict__ goff,
-                                       uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit) {
-    const uint32_t g = (uint32_t)key;
-    point_list[slot] = g;
-    const uint2 r = rects[g];
-    const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF;
-    slot_emit[slot] = goff[g] + (uint32_t)((ty - y0) * (x1 - x0) + (tx - x0));  // y-major emission order
-}
 
 // ---- wave-level register bitonic sort (gfx950 cross-lane ops) ------------------------------
 // Element i = lane * R + r lives in register r of `lane`: exchanges at distance < R stay inside a
@@ -417,8 +420,8 @@ __device__ inline void block_xchg_stage(uint64_t (&k)[R], uint32_t (&v)[R], uint
 // sorted keys in s_key[0, n) and emissions in s_val[0, n).  Keys are (depth_bits << 32 | index),
 // unique inside a tile.
 template <int R, int NW>
-__device__ inline void block_sort_tile(int n, uint32_t start, const uint64_t *__restrict__ keys,
-                                       const uint32_t *__restrict__ vals, uint64_t *s_key, uint32_t *s_val) {
+__device__ inline void block_sort_tile(int n, uint32_t start, const uint4 *__restrict__ pairs, uint64_t *s_key,
+                                       uint32_t *s_val) {
     constexpr int SEG = 64 * R;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t gbase = (uint32_t)(w * SEG), ibase = gbase + lane * R;
@@ -427,8 +430,9 @@ __device__ inline void block_sort_tile(int n, uint32_t start, const uint64_t *__
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int i = (int)ibase + r;
-        k[r] = i < n ? keys[start + i] : ~0ull;  // +inf padding sorts to the end
-        v[r] = i < n ? vals[start + i] : 0u;
+        const uint4 q = i < n ? pairs[start + i] : make_uint4(~0u, ~0u, 0u, 0u);  // +inf padding sorts last
+        k[r] = pair_key(q);
+        v[r] = q.z;
     }
     wave_sort_stages<R, 2>(k, v, lane, gbase);
     for (uint32_t kk = 2 * SEG; kk <= (uint32_t)(NW * SEG); kk <<= 1) {
@@ -445,10 +449,7 @@ __device__ inline void block_sort_tile(int n, uint32_t start, const uint64_t *__
 // lane); beyond that an in-place bitonic network in global memory.
 __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
                                                     const uint2 *__restrict__ ranges,
-                                                    uint64_t *__restrict__ keys,
-                                                    const uint32_t *__restrict__ vals,
-                                                    const uint2 *__restrict__ rects,
-                                                    const uint32_t *__restrict__ goff,
+                                                    uint4 *__restrict__ pairs,
                                                     uint32_t *__restrict__ point_list,
                                                     uint32_t *__restrict__ slot_emit) {
     __shared__ uint64_t s_keys[kSortCap];
@@ -456,12 +457,11 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
     const int tile = (int)tiles[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    const int tx = tile % gx, ty = tile / gx;
     const int tid = threadIdx.x, nt = blockDim.x;
     if (n <= kSortCap) {
         static_assert(kSortCap == 8 * 64 * 8, "k_tile_sort: 8 waves x 64 lanes x 8 keys");
-        if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, keys, vals, s_keys, s_vals);
-        else block_sort_tile<8, 8>(n, rg.x, keys, vals, s_keys, s_vals);
+        if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, pairs, s_keys, s_vals);
+        else block_sort_tile<8, 8>(n, rg.x, pairs, s_keys, s_vals);
         for (int i = tid; i < n; i += nt) {
             point_list[rg.x + i] = (uint32_t)s_keys[i];
             slot_emit[rg.x + i] = s_vals[i];
@@ -469,7 +469,7 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
     } else {
         // long tile: in-place bitonic network in global memory with virtual +inf padding
         // ("flip" form: every comparator puts the minimum at the lower index).
-        uint64_t *a = keys + rg.x;
+        uint4 *a = pairs + rg.x;
         int np = 1;
         while (np < n) np <<= 1;
         for (int k = 2; k <= np; k <<= 1) {
@@ -477,8 +477,8 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
             for (int i = tid; i < (np >> 1); i += nt) {
                 const int lo = ((i & ~(h - 1)) << 1) | (i & (h - 1)), hi = lo ^ (k - 1);
                 if (hi < n) {
-                    const uint64_t x = a[lo], y = a[hi];
-                    if (x > y) { a[lo] = y; a[hi] = x; }
+                    const uint4 x = a[lo], y = a[hi];
+                    if (pair_key(x) > pair_key(y)) { a[lo] = y; a[hi] = x; }
                 }
             }
             __syncthreads();
@@ -486,14 +486,18 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
                 for (int i = tid; i < (np >> 1); i += nt) {
                     const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
                     if (hi < n) {
-                        const uint64_t x = a[lo], y = a[hi];
-                        if (x > y) { a[lo] = y; a[hi] = x; }
+                        const uint4 x = a[lo], y = a[hi];
+                        if (pair_key(x) > pair_key(y)) { a[lo] = y; a[hi] = x; }
                     }
                 }
                 __syncthreads();
             }
         }
-        for (int i = tid; i < n; i += nt) tile_sort_write(a[i], rg.x + i, tx, ty, rects, goff, point_list, slot_emit);
+        for (int i = tid; i < n; i += nt) {
+            const uint4 q = a[i];
+            point_list[rg.x + i] = q.x;
+            slot_emit[rg.x + i] = q.z;
+        }
     }
 }
 
@@ -508,7 +512,7 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
 // set; saturated quarters skip their evaluations and the walk ends when all four are saturated.
 __global__ __launch_bounds__(256) void k_render_fwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
-    const uint64_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+    const uint4 *__restrict__ pairs,
     uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
     float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
@@ -530,9 +534,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const int n = (int)(rg.y - rg.x);
     const bool sorted_here = n <= kFwdSortCap;
     if (n > 0 && sorted_here) {
-        if (n <= 256) block_sort_tile<1, 4>(n, rg.x, keys, vals, s_key, s_u.val);
-        else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, keys, vals, s_key, s_u.val);
-        else block_sort_tile<4, 4>(n, rg.x, keys, vals, s_key, s_u.val);
+        if (n <= 256) block_sort_tile<1, 4>(n, rg.x, pairs, s_key, s_u.val);
+        else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, pairs, s_key, s_u.val);
+        else block_sort_tile<4, 4>(n, rg.x, pairs, s_key, s_u.val);
         for (int i = threadIdx.x; i < n; i += 256) {
             point_list[rg.x + i] = (uint32_t)s_key[i];
             slot_emit[rg.x + i] = s_u.val[i];
@@ -683,23 +687,23 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
+        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K);
     else
-        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.keys, a.vals, (uint32_t)K);
+        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_long, hipStream_t s) {
     // lists of up to kFwdSortCap pairs are sorted inside k_render_fwd; only longer ones here
     if (n_long == 0) return hipSuccess;
-    k_tile_sort<<<n_long, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.keys, a.vals, a.rect, a.goff,
+    k_tile_sort<<<n_long, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs,
                                         a.point_list, a.slot_emit);
     return hipGetLastError();
 }
 
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
-    k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.keys, a.vals,
+    k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                                    a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.final_T, a.n_contrib,
                                    a.tile_maxc, a.tile_cost);
     return hipGetLastError();
@@ -723,5 +727,8 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 #ifdef GSR_TRACE
 extern "C" int gsr_debug_trace_fwd(void *buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_trace_fwd), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
+}
+extern "C" int gsr_debug_trace_emit(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(gsr::g_trace_emit), &buf, sizeof(buf)) == hipSuccess ? 0 : 2;
 }
 #endif

@@ -22,7 +22,7 @@ struct FwdArgs {
     uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
     // binning
-    uint64_t *keys; uint32_t *vals; uint32_t *point_list; uint32_t *slot_emit;
+    uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit;
     // outputs
     int *radii; float *out_color; float *out_depth;
 };

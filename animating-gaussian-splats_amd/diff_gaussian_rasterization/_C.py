@@ -320,7 +320,9 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
         "final_T": view(imgBuffer, o[6], W * H, f32, (H, W)),
         "n_contrib": view(imgBuffer, o[7], W * H, i32, (H, W)),
         "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
-        "keys": view(binningBuffer, o[9], K, i64, (K,)),
+        # per-pair records (index, depth bits, emission, 0) in tile-bucket order; keys = .x | .y << 32
+        "pairs": view(binningBuffer, o[9], 4 * K, i32, (K, 4)),
+        "keys": view(binningBuffer, o[9], 2 * K, i64, (K, 2))[:, 0],
         "point_list": view(binningBuffer, o[10], K, i32, (K,)),
         "slot_emit": view(binningBuffer, o[11], K, i32, (K,)),
     }

@@ -149,7 +149,7 @@ size_t gsr_scratch_bytes(int num_rendered);
 
 /* Introspection for parity tests: byte offsets of the arrays inside the three forward buffers, in
  * this order: geom {depth, rec (64-byte render records), rect, tiles, goff}, image {ranges,
- * final_T, n_contrib, tile_maxc}, binning {keys, point_list, slot_emit}.  Returns the count written (12). */
+ * final_T, n_contrib, tile_maxc}, binning {pairs (16-byte records: index, depth bits, emission, 0), point_list, slot_emit}.  Returns the count written (12). */
 int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *out, int max_out);
 
 const char *gsr_last_error(void);

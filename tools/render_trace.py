@@ -44,6 +44,23 @@ def analyse(buf, n_waves, label):
     return out
 
 
+def analyse_emit(buf, label):
+    """k_bin_emit per-block stamps (start, LDS count done, slabs reserved, end), microseconds."""
+    a = buf.reshape(-1, 4).astype(np.int64)
+    a = a[a[:, 0] > 0]
+    if not len(a):
+        return {}
+    t0 = a[:, 0].min()
+    rel = (a - t0) / 100.0
+    ph = np.diff(rel, axis=1)  # count, reserve, scatter
+    pct = lambda x: [round(float(np.percentile(x, q)), 1) for q in (50, 90, 100)]  # noqa: E731
+    out = {"blocks": int(len(a)), "span_us": round(float(rel[:, 3].max()), 1),
+           "start_us_p50_p90_max": pct(rel[:, 0]), "count_us": pct(ph[:, 0]), "reserve_us": pct(ph[:, 1]),
+           "scatter_us": pct(ph[:, 2])}
+    print(f"[{label}] " + json.dumps(out))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
@@ -70,18 +87,22 @@ def main():
     bbuf = torch.zeros(3 * 4 * T, dtype=torch.int64, device=dev)
     L.gsr_debug_trace_fwd.argtypes = [ctypes.c_void_p]
     L.gsr_debug_trace_bwd.argtypes = [ctypes.c_void_p]
+    L.gsr_debug_trace_emit.argtypes = [ctypes.c_void_p]
+    ebuf = torch.zeros(4 * 4096, dtype=torch.int64, device=dev)
     for ci in [int(c) for c in args.cams.split(",")]:  # warm-up
         GaussianRasterizer(raster_settings=cams[ci])(**leaves)[0].backward(dl)
     torch.cuda.synchronize()
     report = {}
     for ci in [int(c) for c in args.cams.split(",")]:
-        fbuf.zero_(); bbuf.zero_()
+        fbuf.zero_(); bbuf.zero_(); ebuf.zero_()
         assert L.gsr_debug_trace_fwd(fbuf.data_ptr()) == 0 and L.gsr_debug_trace_bwd(bbuf.data_ptr()) == 0
+        assert L.gsr_debug_trace_emit(ebuf.data_ptr()) == 0
         img, radii, _ = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
         img.backward(dl)
         torch.cuda.synchronize()
-        L.gsr_debug_trace_fwd(None); L.gsr_debug_trace_bwd(None)
-        report[ci] = {"fwd": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd"),
+        L.gsr_debug_trace_fwd(None); L.gsr_debug_trace_bwd(None); L.gsr_debug_trace_emit(None)
+        report[ci] = {"emit": analyse_emit(ebuf.cpu().numpy(), f"cam{ci} emit"),
+                      "fwd": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd"),
                       "bwd": analyse(bbuf.cpu().numpy(), T, f"cam{ci} bwd")}
     out = os.path.join(REPO, "gpurun_out")
     os.makedirs(out, exist_ok=True)
