@@ -13,6 +13,8 @@
 #include "gsr_common.h"
 #include "gsr_internal.h"
 
+#include <algorithm>
+
 namespace gsr {
 
 #ifdef GSR_TRACE
@@ -50,7 +52,7 @@ __global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *
 // the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
 // quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour)
 // with the exact conic, storing one 36-byte record per sorted slot (coalesced, no atomics).
-__global__ __launch_bounds__(256) void k_render_bwd(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_render_bwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
     const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
@@ -58,8 +60,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
     float4 *__restrict__ part) {
     __shared__ float4 s_rec[kTilesPerBlock][3][64];
-    __shared__ float s_outs[kTilesPerBlock][64 * 2 * kPartial];  // two halves per sum
-    __shared__ uint32_t s_qs[kTilesPerBlock][64];
+    __shared__ float s_outs[kTilesPerBlock][64 * kPartial];  // per staged pair: its kPartial wave sums
     const int wv = threadIdx.x >> 6;
     const int t_lin = blockIdx.x * kTilesPerBlock + wv;
     if (t_lin >= T) return;
@@ -70,7 +71,6 @@ __global__ __launch_bounds__(256) void k_render_bwd(
     float4(&s_b)[64] = s_rec[wv][1];
     float4(&s_c)[64] = s_rec[wv][2];
     float *s_out = s_outs[wv];
-    uint32_t *s_q = s_qs[wv];
     const int tile = (int)tile_order[t_lin];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         const int start = end > 64 ? end - 64 : 0;
         const int cnt = end - start;
 #pragma unroll
-        for (int q = 0; q < 2 * kPartial; ++q) s_out[lane * 2 * kPartial + q] = 0.f;
+        for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
         // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile; a
         // quarter whose pixels all precede this slot in the forward's order (p >= its max
         // n_contrib) is skipped too
@@ -138,27 +138,28 @@ __global__ __launch_bounds__(256) void k_render_bwd(
             const uint32_t g = point_list[rg.x + p];
             g_st = g;
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
-            s_a[lane] = a; s_b[lane] = b; s_c[lane] = c;
+            s_a[lane] = a; s_b[lane] = b;
             const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (p < qmax[k] &&
                     !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0 + 4 * k, tx1, ty0 + 4 * k + 3))
                     qmask |= 1u << k;
+            s_c[lane] = make_float4(c.x, c.y, c.z, __uint_as_float(qmask));  // .w: the quarter mask
         }
-        s_q[lane] = qmask;
         uint64_t m = __ballot(qmask != 0);
         wave_lds_sync();
         while (m) {
             const int j = 63 - __builtin_clzll(m);
             m &= ~(1ull << j);
             const uint32_t p = (uint32_t)(start + j);
-            const uint32_t qm = __builtin_amdgcn_readfirstlane(s_q[j]);  // wave-uniform quarter mask
             const float4 a = s_a[j], b = s_b[j], c = s_c[j];
+            const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));  // wave-uniform quarter mask
             const PairX x = pair_x(a, pfx);
             // per-lane sums over this lane's pixels: S0 = sum G dL/dalpha, S1 = sum G dL/dalpha dy,
             // S4 = sum G dL/dalpha dy^2, cs = sum alpha T dL/dpix (the lane's 4 pixels share dx)
-            float S0 = 0.f, S1 = 0.f, S4 = 0.f, cs0 = 0.f, cs1 = 0.f, cs2 = 0.f;
+            // -0 seeds: x + (-0) == x for every x, so the first contributor needs no add (the ISA folds it)
+            float S0 = -0.f, S1 = -0.f, S4 = -0.f, cs0 = -0.f, cs1 = -0.f, cs2 = -0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -191,11 +192,12 @@ __global__ __launch_bounds__(256) void k_render_bwd(
             if (__ballot(any)) {
                 // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
                 const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
-                if ((lane & 15) < 2) {  // lanes 0 and 1 of each row: the two halves of its sums
-                    float *o2 = s_out + j * 2 * kPartial + (lane & 1);
-                    o2[2 * xslot] = sm.X;
-                    o2[2 * yslot] = sm.Y;
-                    if (lane < 2) o2[2 * 5] = sm.Z;
+                if ((lane & 15) < 2) {  // lanes 0 and 1 of each row hold the two halves of its sums:
+                    // both are added into the zeroed slot, 0 + h0 + h1 == h0 + h1 in either order
+                    float *o = s_out + j * kPartial;
+                    lds_add(o + xslot, sm.X);
+                    lds_add(o + yslot, sm.Y);
+                    if (lane < 2) lds_add(o + 5, sm.Z);
                 }
             }
         }
@@ -203,10 +205,10 @@ __global__ __launch_bounds__(256) void k_render_bwd(
         if (lane < cnt) {
             const float4 cj = rec[(size_t)kRecF4 * g_st + 3];  // exact conic (a, b, c)
             const uint32_t em = slot_emit[rg.x + start + lane];
-            const float *s2 = s_out + lane * 2 * kPartial;
+            const float *s2 = s_out + lane * kPartial;
             float sm[kPartial];
 #pragma unroll
-            for (int q = 0; q < kPartial; ++q) sm[q] = s2[2 * q] + s2[2 * q + 1];
+            for (int q = 0; q < kPartial; ++q) sm[q] = s2[q];
             const float o = s_b[lane].y;  // the moments of sG = opacity G dL/dalpha
             const float S1 = o * sm[0], S2 = o * sm[1];
             float4 *dst = part + 3 * (size_t)em;
@@ -352,6 +354,47 @@ __device__ inline void cov3d_backward(float3 s3, float mod, float4 q, const floa
 #undef G
 }
 
+// Records summed per Gaussian, staged through LDS: the 64 Gaussians of a wave own the contiguous
+// record span [goff[first], goff[last + 1]) (emission order), which the wave reads in chunks of
+// kRecChunk records with lane-contiguous float4 loads (a handful of lines per load instruction instead
+// of one line per lane), parks in its LDS slice, and every lane then adds its own records from LDS
+// in emission order -- the same additions in the same order as a direct per-lane walk.
+// kRecChunk: 256 records when the SH rows' LDS slice of a wave holds them (MC = 16), else 128.
+template <int MC> constexpr int kRecChunk = 3 * 256 * 16 <= 64 * sh_row_stride(MC) * 4 ? 256 : 128;
+template <int MC> constexpr int kRecStageF4 = 3 * kRecChunk<MC>;  // float4 per wave slice
+template <int MC>
+__device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict__ goff,
+                                        const float4 *__restrict__ part, float4 *stage,
+                                        float (&acc)[kPartial]) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t e0 = goff[i < P ? i : P], e1 = i < P ? goff[i + 1] : e0;
+    const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0);
+    const uint32_t E1 = __builtin_amdgcn_readlane(e1, 63);
+#pragma unroll
+    for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
+    constexpr int C = kRecChunk<MC>, NF4 = kRecStageF4<MC>;
+    for (uint32_t cb = E0; cb < E1; cb += C) {
+        const uint32_t n3 = 3u * min((uint32_t)C, E1 - cb);
+        const float4 *src = part + 3 * (size_t)cb;
+        float4 v[NF4 / 64];
+#pragma unroll
+        for (int t = 0; t < NF4 / 64; ++t)  // clamped index: every load in bounds, none predicated
+            v[t] = src[min(lane + 64u * t, n3 - 1u)];
+#pragma unroll
+        for (int t = 0; t < NF4 / 64; ++t)
+            if (lane + 64u * t < n3) stage[lane + 64 * t] = v[t];
+        wave_lds_sync();
+        const uint32_t a = max(e0, cb), b = min(e1, cb + C);
+        for (uint32_t e = a; e < b; ++e) {
+            const float4 pa = stage[3 * (e - cb)], pb = stage[3 * (e - cb) + 1];
+            const float pc = reinterpret_cast<const float *>(stage + 3 * (e - cb) + 2)[0];
+            acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
+            acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc;
+        }
+        wave_lds_sync();
+    }
+}
+
 template <int MC>
 __device__ inline void gauss_bwd_one(
     int i, int D, int M, int W, int H, float scale_modifier, float tan_fovx, float tan_fovy,
@@ -359,8 +402,7 @@ __device__ inline void gauss_bwd_one(
     const float *__restrict__ rotations, const float *__restrict__ shs,
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
     const float *__restrict__ projmatrix, const float *__restrict__ campos,
-    const int *__restrict__ radii, const uint32_t *__restrict__ goff,
-    const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
+    const int *__restrict__ radii, const float (&acc)[kPartial], float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec, int accm) {
@@ -393,16 +435,6 @@ __device__ inline void gauss_bwd_one(
             for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
         }
         return;
-    }
-    // ---- sum this Gaussian's pair records (contiguous, emission order) ----
-    float acc[kPartial];
-#pragma unroll
-    for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
-    const uint32_t e0 = goff[i], e1 = goff[i + 1];
-    for (uint32_t e = e0; e < e1; ++e) {
-        const float4 pa = part[3 * (size_t)e], pb = part[3 * (size_t)e + 1], pc = part[3 * (size_t)e + 2];
-        acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
-        acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc.x;
     }
     gput(dL_dmeans2D, 3 * i, acc[0], a2); gput(dL_dmeans2D, 3 * i + 1, acc[1], a2); gput(dL_dmeans2D, 3 * i + 2, 0.f, a2);
     // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
@@ -557,14 +589,18 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
     const int nrow = min(kShBlock, P - i0);
+    const int i = i0 + threadIdx.x;
+    // the record sums first, each wave in its own slice of the block's LDS (which the SH rows reuse)
+    float acc[kPartial];
+    sum_records_wave<MC>(i, P, goff, part, reinterpret_cast<float4 *>(s_sh) + (threadIdx.x >> 6) * kRecStageF4<MC>, acc);
     if constexpr (MC > 0) {  // coalesced copy of this block's SH rows into LDS (reused for dL/dSH)
+        __syncthreads();
         sh_rows_to_lds<MC>(shs + (size_t)i0 * RL, nrow, s_sh);
         __syncthreads();
     }
-    const int i = i0 + threadIdx.x;
     if (i < P) gauss_bwd_one<MC>(i, D, M, W, H, scale_modifier, tan_fovx, tan_fovy, h_x, h_y, means3D,
                                  scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos,
-                                 radii, goff, part, dL_dmeans2D, dL_dcolors, dL_dopacity,
+                                 radii, acc, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
                                  act, rec, accm);
     if constexpr (MC > 0) {  // coalesced store of the dL/dSH rows
@@ -589,7 +625,9 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
 
 template <int MC>
 static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
-    k_gauss_bwd<MC><<<div_up(a.P, kShBlock), kShBlock, sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0), s>>>(
+    constexpr size_t lds = std::max(sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0),
+                                    sizeof(float4) * kRecStageF4<MC> * (kShBlock / 64));
+    k_gauss_bwd<MC><<<div_up(a.P, kShBlock), kShBlock, lds, s>>>(
         a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
         a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
         a.radii, a.goff, a.part, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,

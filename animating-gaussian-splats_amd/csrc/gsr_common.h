@@ -126,31 +126,36 @@ __host__ __device__ constexpr int sh_row_stride(int MC) { return (3 * MC) | 1; }
 
 // Block copy of `nrow` SH rows (3 MC floats each, contiguous in global memory) into LDS rows of
 // stride sh_row_stride(MC).  The block's global span starts 16-byte aligned whenever the array does
-// (kShBlock * 3 MC is a multiple of 4), so it is read as float4: every thread issues all its loads
-// before its first LDS store (up to 12 in flight per lane for MC = 16).
-template <int MC>
+// (kShBlock * 3 MC is a multiple of 4), so it is read as float4: every thread issues up to INFL loads
+// before its first LDS store (all 12 at once for MC = 16 by default; a caller with live registers
+// passes a smaller INFL and the copy runs in rounds).
+template <int MC, int INFL = 16>
 __device__ inline void sh_rows_to_lds(const float *__restrict__ src, int nrow, float *s) {
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     constexpr int IT = (kShBlock * RL / 4 + kShBlock - 1) / kShBlock;
+    constexpr int B = IT < INFL ? IT : INFL;
     const int n = nrow * RL;
     if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
         const int n4 = n >> 2;
         const float4 *s4 = reinterpret_cast<const float4 *>(src);
-        float4 v[IT];
 #pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int q = threadIdx.x + it * kShBlock;
-            if (q < n4) v[it] = s4[q];
-        }
+        for (int i0 = 0; i0 < IT; i0 += B) {
+            float4 v[B];
 #pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int q = threadIdx.x + it * kShBlock;
-            if (q < n4) {
-                const float f[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+            for (int it = 0; it < B; ++it) {
+                const int q = threadIdx.x + (i0 + it) * kShBlock;
+                if (i0 + it < IT && q < n4) v[it] = s4[q];
+            }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = 4 * q + j, r = e / RL;
-                    s[r * RS + (e - r * RL)] = f[j];
+            for (int it = 0; it < B; ++it) {
+                const int q = threadIdx.x + (i0 + it) * kShBlock;
+                if (i0 + it < IT && q < n4) {
+                    const float f[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 4 * q + j, r = e / RL;
+                        s[r * RS + (e - r * RL)] = f[j];
+                    }
                 }
             }
         }
@@ -571,6 +576,11 @@ __device__ inline bool tile_cull(float gx, float gy, float a, float b, float c, 
 //   r4567: lane 0 -> v4, lane 16 -> v6, lane 32 -> v5, lane 48 -> v7
 //   r8   : lane 0 -> v8
 // (every lane of a row holds its row's total).  Fixed tree: bitwise reproducible.
+// No-return LDS float add (ds_add_f32).
+__device__ inline void lds_add(float *p, float v) {
+    (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ inline float fold32(float a, float b) {  // lanes 0-31: a folded, lanes 32-63: b folded
     auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
