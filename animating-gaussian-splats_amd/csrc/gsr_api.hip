@@ -156,7 +156,7 @@ void carve_image(FwdArgs &a, char *base) {
     const ImageLayout L(a.W, a.H, a.P);
     a.ranges = (uint2 *)(base + L.ranges); a.final_T = (float *)(base + L.final_T);
     a.n_contrib = (uint32_t *)(base + L.n_contrib); a.tile_maxc = (uint32_t *)(base + L.tile_maxc);
-    a.tile_cost = (uint32_t *)(base + L.tile_cost); a.tile_order_f = (uint32_t *)(base + L.tile_order_f);
+    a.tile_order_f = (uint32_t *)(base + L.tile_order_f);
     a.tile_order_b = (uint32_t *)(base + L.tile_order_b);
     a.sort_lists = (uint32_t *)(base + L.sort_lists);
     a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
@@ -292,7 +292,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.radii = radii;
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff;
     a.ranges = f.ranges; a.final_T = f.final_T; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
-    a.tile_cost = f.tile_cost; a.tile_order_b = f.tile_order_b;
+    a.tile_order_b = f.tile_order_b;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit;
     a.dL_dcolor = dL_dcolor;
     a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;

@@ -21,9 +21,12 @@ namespace gsr {
 __device__ uint64_t *g_trace_bwd;
 #endif
 
-// Backward dispatch order (one block): tiles by descending sum of n_contrib over their pixels.
-__global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *__restrict__ tile_cost,
-                                                         uint32_t *__restrict__ tile_order) {
+// Backward dispatch order (one block): tiles by descending sum of their quarters' max n_contrib (the
+// pairs each quarter walks: the per-pair evaluations and reductions follow it far more closely than
+// the sum of n_contrib over the pixels), laid out boustrophedon over rounds of one wave per SIMD.
+__global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *__restrict__ tile_maxc,
+                                                         uint32_t *__restrict__ tile_order, int simds) {
+    const SnakePos pos{(uint32_t)max(simds, 1), (uint32_t)T};
     __shared__ uint32_t s_red[16];
     __shared__ uint32_t s_hist[kOrderBuckets];
     if (T <= kScanRegs * (int)blockDim.x) {  // costs prefetched into registers, all loads in flight
@@ -32,16 +35,16 @@ __global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *
 #pragma unroll
         for (int i = 0; i < kScanRegs; ++i) {
             uint4 q = make_uint4(0, 0, 0, 0);
-            if (i < c && t0 + i < T) q = reinterpret_cast<const uint4 *>(tile_cost)[t0 + i];
+            if (i < c && t0 + i < T) q = reinterpret_cast<const uint4 *>(tile_maxc)[t0 + i];
             cost[i] = q.x + q.y + q.z + q.w;
         }
-        lpt_order_regs<kScanRegs>(T, c, cost, tile_order, s_hist, s_red);
+        lpt_order_regs<kScanRegs>(T, c, cost, tile_order, s_hist, s_red, pos);
         return;
     }
     lpt_order(T, [&](int t) {
-        const uint4 c = reinterpret_cast<const uint4 *>(tile_cost)[t];
+        const uint4 c = reinterpret_cast<const uint4 *>(tile_maxc)[t];
         return c.x + c.y + c.z + c.w;
-    }, tile_order, s_hist, s_red);
+    }, tile_order, s_hist, s_red, pos);
 }
 
 // One wave64 per tile, 4 pixels per lane, reverse walk over the tile's list in batches of 64;
@@ -52,20 +55,18 @@ __global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *
 // the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
 // quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour)
 // with the exact conic, storing one 36-byte record per sorted slot (coalesced, no atomics).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_render_bwd(
-    int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
+__device__ __forceinline__ void render_bwd_tile(
+    int t_lin, int W, int H, int gx, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
     const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
-    float4 *__restrict__ part) {
-    __shared__ float4 s_rec[kTilesPerBlock][3][64];
-    __shared__ float s_outs[kTilesPerBlock][64 * kPartial];  // per staged pair: its kPartial wave sums
+    float4 *__restrict__ part, float4 (&s_rec)[kTilesPerBlock][3][64],
+    float (&s_outs)[kTilesPerBlock][64 * kPartial]) {
     const int wv = threadIdx.x >> 6;
-    const int t_lin = blockIdx.x * kTilesPerBlock + wv;
-    if (t_lin >= T) return;
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint32_t tr_evals = 0, tr_reds = 0;  // (pair, quarter) evaluations and wave reductions
 #endif
     float4(&s_a)[64] = s_rec[wv][0];
     float4(&s_b)[64] = s_rec[wv][1];
@@ -189,6 +190,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
                 cs1 = fmaf(dch, dp1[k], cs1);
                 cs2 = fmaf(dch, dp2[k], cs2);
             }
+#ifdef GSR_TRACE
+            tr_evals += __builtin_popcount(qm);
+            tr_reds += __ballot(any) ? 1u : 0u;
+#endif
             if (__ballot(any)) {
                 // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
                 const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
@@ -221,8 +226,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
         }
     }
 #ifdef GSR_TRACE
-    trace_wave(g_trace_bwd, t_lin, t_start);
+    trace_wave(g_trace_bwd, t_lin, t_start, tr_evals | ((uint64_t)tr_reds << 32));
 #endif
+}
+
+// One wave per tile, 4 tiles per block, every wave resident at once on MI355X (<= 6144 slots): the
+// order (k_tile_order_bwd) decides which SIMD holds which tiles, so it is an LPT list laid out
+// boustrophedon over rounds of one wave per SIMD (SnakePos) to even out each SIMD's total.
+__global__ __launch_bounds__(256) void k_render_bwd(
+    int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
+    const uint32_t *__restrict__ point_list,
+    const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
+    const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
+    const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
+    float4 *__restrict__ part) {
+    __shared__ float4 s_rec[kTilesPerBlock][3][64];
+    __shared__ float s_outs[kTilesPerBlock][64 * kPartial];  // per staged pair: its kPartial wave sums
+    const int t_lin = (int)blockIdx.x * kTilesPerBlock + (int)(threadIdx.x >> 6);
+    if (t_lin < T)
+        render_bwd_tile(t_lin, W, H, gx, tile_order, ranges, point_list, rec, bg, final_Ts, n_contrib,
+                        tile_maxc, slot_emit, dL_dpixels, part, s_rec, s_outs);
 }
 
 // Gradient output write: plain store, or (accumulate bit set, gsr_grads.accumulate) add into the
@@ -612,10 +635,23 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 
 
 // ==========================================================================================
+// SIMDs of the current device (CUs x 4), cached per device: the round size of the backward's order.
+static int device_simds() {
+    static int cache[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+    if (!cache[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        cache[dev] = 4 * cus;
+    }
+    return cache[dev];
+}
+
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (a.K == 0) return hipSuccess;
-    k_tile_order_bwd<<<1, 1024, 0, s>>>(T, a.tile_cost, a.tile_order_b);
+    k_tile_order_bwd<<<1, 1024, 0, s>>>(T, a.tile_maxc, a.tile_order_b, device_simds());
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     k_render_bwd<<<div_up(T, kTilesPerBlock), 64 * kTilesPerBlock, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_b, a.ranges, a.point_list, a.rec, a.bg, a.final_T,

@@ -66,7 +66,7 @@ struct BinGrid {
 
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
 struct ImageLayout {
-    size_t ranges, final_T, n_contrib, tile_maxc, tile_cost, tile_order_f, tile_order_b, sort_lists,
+    size_t ranges, final_T, n_contrib, tile_maxc, tile_order_f, tile_order_b, sort_lists,
         tile_count, tile_cursor, block_sums, block_off, meta, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
@@ -77,7 +77,6 @@ struct ImageLayout {
         final_T = o;     o = align256(o + sizeof(float) * N);
         n_contrib = o;   o = align256(o + sizeof(uint32_t) * N);
         tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter tile (16x4 px)
-        tile_cost = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter: sum of n_contrib
         tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
         tile_order_b = o; o = align256(o + sizeof(uint32_t) * T);    // backward dispatch order (LPT)
         sort_lists = o;  o = align256(o + sizeof(uint32_t) * T);      // tiles longer than kFwdSortCap
@@ -407,11 +406,14 @@ constexpr int kTilesPerBlock = 4;
 // HW_ID) with s_memrealtime (100 MHz, chip-wide) into a buffer registered by
 // gsr_debug_trace_{fwd,bwd}; compiled out of libgsr.so.
 #ifdef GSR_TRACE
-__device__ inline void trace_wave(uint64_t *buf, int slot, uint64_t t0) {
+// per wave: start, end, HW_ID | XCC_ID << 32, kernel-defined work counter
+__device__ inline void trace_wave(uint64_t *buf, int slot, uint64_t t0, uint64_t work = 0) {
     if (buf && (threadIdx.x & 63) == 0) {
-        buf[3 * slot] = t0;
-        buf[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
-        buf[3 * slot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+        buf[4 * slot] = t0;
+        buf[4 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+        buf[4 * slot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |     // HW_REG_HW_ID
+                            ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);  // HW_REG_XCC_ID
+        buf[4 * slot + 3] = work;
     }
 }
 #endif
@@ -457,9 +459,10 @@ __device__ inline void wave_lds_sync() {
 // by descending cost(t) (bucketed into 2048 log-free linear buckets; arbitrary order inside a bucket,
 // which only affects scheduling).  `s_hist` must hold 2048 words, `s_red` 16.  All threads call it.
 constexpr int kOrderBuckets = 2048;
-template <typename CostFn>
+struct IdentityPos { __device__ uint32_t operator()(uint32_t p) const { return p; } };
+template <typename CostFn, typename PosMap = IdentityPos>
 __device__ inline void lpt_order(int T, CostFn cost, uint32_t *__restrict__ order, uint32_t *s_hist,
-                                 uint32_t *s_red) {
+                                 uint32_t *s_red, PosMap pos = PosMap()) {
     uint32_t mx = 0;
     for (int t = threadIdx.x; t < T; t += blockDim.x) mx = max(mx, cost(t));
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
@@ -485,15 +488,15 @@ __device__ inline void lpt_order(int T, CostFn cost, uint32_t *__restrict__ orde
     }
     __syncthreads();
     for (int t = threadIdx.x; t < T; t += blockDim.x)
-        order[atomicAdd(&s_hist[kOrderBuckets - 1 - (cost(t) >> shift)], 1u)] = (uint32_t)t;
+        order[pos(atomicAdd(&s_hist[kOrderBuckets - 1 - (cost(t) >> shift)], 1u))] = (uint32_t)t;
 }
 
 // The same LPT order when every thread already holds the costs of the c consecutive tiles
 // t = threadIdx.x * c + i (i < c <= C) in registers: the single-block scan kernels prefetch them with
 // every load in flight instead of re-reading global memory in dependent strided loops.
-template <int C>
+template <int C, typename PosMap = IdentityPos>
 __device__ inline void lpt_order_regs(int T, int c, const uint32_t (&cost)[C], uint32_t *__restrict__ order,
-                                      uint32_t *s_hist, uint32_t *s_red) {
+                                      uint32_t *s_hist, uint32_t *s_red, PosMap pos = PosMap()) {
     const int t0 = threadIdx.x * c;
     uint32_t mx = 0;
 #pragma unroll
@@ -525,8 +528,23 @@ __device__ inline void lpt_order_regs(int T, int c, const uint32_t (&cost)[C], u
 #pragma unroll
     for (int i = 0; i < C; ++i)
         if (i < c && t0 + i < T)
-            order[atomicAdd(&s_hist[kOrderBuckets - 1 - (cost[i] >> shift)], 1u)] = (uint32_t)(t0 + i);
+            order[pos(atomicAdd(&s_hist[kOrderBuckets - 1 - (cost[i] >> shift)], 1u))] = (uint32_t)(t0 + i);
 }
+// Boustrophedon over rounds of S slots: rank p of round r = p / S lands at slot p % S in even rounds and
+// at the mirrored slot in odd ones (the last, partial round mirrors within its own length).  For a
+// launch whose waves are all resident at once (one wave per SIMD per round, S = SIMDs), each SIMD
+// then holds one heavy and one light tile of every pair of rounds instead of the k-th heaviest of
+// every round.
+struct SnakePos {
+    uint32_t S, T;
+    __device__ uint32_t operator()(uint32_t p) const {
+        const uint32_t r = p / S, j = p - r * S;
+        if (!(r & 1u)) return p;
+        const uint32_t L = min(S, T - r * S);
+        return r * S + (L - 1u - j);
+    }
+};
+
 // Tiles per thread held in registers by the single-block kernels (1024 threads): T <= 16384.
 constexpr int kScanRegs = 16;
 

@@ -47,11 +47,22 @@ __global__ __launch_bounds__(256) void k_preprocess(
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
+    const int i = i0 + threadIdx.x;
+    // this Gaussian's own inputs are loaded first (clamped index for the tail lanes), so their
+    // latency overlaps the SH row copy instead of following its barrier
+    const int ic = min(i, P - 1);
+    const float3 p = make_float3(means3D[3 * ic], means3D[3 * ic + 1], means3D[3 * ic + 2]);
+    float3 s_in = make_float3(0.f, 0.f, 0.f);
+    float4 q_in = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!cov3D_precomp) {
+        s_in = make_float3(scales[3 * ic], scales[3 * ic + 1], scales[3 * ic + 2]);
+        q_in = make_float4(rotations[4 * ic], rotations[4 * ic + 1], rotations[4 * ic + 2], rotations[4 * ic + 3]);
+    }
+    const float o_in = opacities[ic];
     if constexpr (MC > 0) {  // coalesced copy of this block's SH rows into LDS
         sh_rows_to_lds<MC>(shs + (size_t)i0 * RL, min(kShBlock, P - i0), s_sh);
         __syncthreads();
     }
-    const int i = i0 + threadIdx.x;
     if (i >= P) return;
     // matrices are tiny and uniform: every lane reads the same words (scalar loads)
     float vm[16], pm[16];
@@ -60,7 +71,6 @@ __global__ __launch_bounds__(256) void k_preprocess(
     radii[i] = 0;
     tiles_out[i] = 0;
     rect_out[i] = make_uint2(0, 0);
-    const float3 p = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     const float4 ph = xform4x4(p, pm);
     const float3 pv = xform4x3(p, vm);
     if (pv.z <= 0.2f) return;  // near-plane cull (in_frustum)
@@ -71,9 +81,8 @@ __global__ __launch_bounds__(256) void k_preprocess(
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = cov3D_precomp[6 * i + k];
     } else {
-        float3 s = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-        float4 q = make_float4(rotations[4 * i], rotations[4 * i + 1], rotations[4 * i + 2],
-                               rotations[4 * i + 3]);
+        float3 s = s_in;
+        float4 q = q_in;
         if (act & GSR_ACT_EXP_SCALES) s = act_exp3(s);
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) q = act_normalize(q, quat_norm(q));
         cov3d_from_scale_rot(s, scale_modifier, q, c3);
@@ -100,7 +109,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
-    const float o = (act & GSR_ACT_SIGMOID_OPACITY) ? act_sigmoid(opacities[i]) : opacities[i];
+    const float o = (act & GSR_ACT_SIGMOID_OPACITY) ? act_sigmoid(o_in) : o_in;
     const float ca = cv.z * det_inv, cb = -cv.y * det_inv, cc = cv.x * det_inv;
     const float tau2 = o >= 1.0f / 255.0f ? 2.f * log2f(255.f * o) : -1.f;
     float4 *r = rec_out + (size_t)kRecF4 * i;
@@ -515,8 +524,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const uint4 *__restrict__ pairs,
     uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
-    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
-    uint32_t *__restrict__ tile_cost) {
+    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc) {
     __shared__ uint64_t s_key[kFwdSortCap];
     __shared__ union {
         uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
@@ -609,13 +617,10 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         out_color[2 * H * W + pid] = C2 + Tt * bg[2];
         out_depth[pid] = Dp;
     }
-    uint32_t mx = last, sum = last;
+    uint32_t mx = last;
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) {
-        mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
-        sum += (uint32_t)__shfl_xor((int)sum, d, 64);
-    }
-    if (lane == 0) { tile_maxc[4 * tile + wv] = mx; tile_cost[4 * tile + wv] = sum; }
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+    if (lane == 0) tile_maxc[4 * tile + wv] = mx;
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
 #endif
@@ -705,7 +710,7 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                                    a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.final_T, a.n_contrib,
-                                   a.tile_maxc, a.tile_cost);
+                                   a.tile_maxc);
     return hipGetLastError();
 }
 

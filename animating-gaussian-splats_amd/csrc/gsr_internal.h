@@ -18,7 +18,7 @@ struct FwdArgs {
     // geom
     float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff;
     // image
-    uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc; uint32_t *tile_cost;
+    uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc;
     uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
     // binning
@@ -36,7 +36,7 @@ struct BwdArgs {
     // saved state
     const float4 *rec; const uint2 *rect;
     const uint32_t *goff; const uint2 *ranges; const float *final_T; const uint32_t *n_contrib;
-    const uint32_t *tile_maxc; const uint32_t *tile_cost; uint32_t *tile_order_b;
+    const uint32_t *tile_maxc; uint32_t *tile_order_b;
     const uint32_t *point_list; const uint32_t *slot_emit;
     // scratch
     float4 *part;

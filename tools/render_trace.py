@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 
 def analyse(buf, n_waves, label):
-    a = buf[: 3 * n_waves].reshape(n_waves, 3).astype(np.int64)
+    a = buf[: 4 * n_waves].reshape(n_waves, 4).astype(np.int64)
     a = a[a[:, 0] > 0]
     if not len(a):
         return {}
@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--cams", default="5,6,7,8")
     args = ap.parse_args()
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     import splat_scenes as S
     from diff_gaussian_rasterization import GaussianRasterizer, _C
     L = _C.load_library()
@@ -83,8 +84,8 @@ def main():
     cams = S.scene_cameras(cfg, device=dev)
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
-    fbuf = torch.zeros(3 * 4 * T, dtype=torch.int64, device=dev)
-    bbuf = torch.zeros(3 * 4 * T, dtype=torch.int64, device=dev)
+    fbuf = torch.zeros(4 * 4 * T, dtype=torch.int64, device=dev)
+    bbuf = torch.zeros(4 * 4 * T, dtype=torch.int64, device=dev)
     L.gsr_debug_trace_fwd.argtypes = [ctypes.c_void_p]
     L.gsr_debug_trace_bwd.argtypes = [ctypes.c_void_p]
     L.gsr_debug_trace_emit.argtypes = [ctypes.c_void_p]
@@ -101,6 +102,7 @@ def main():
         img.backward(dl)
         torch.cuda.synchronize()
         L.gsr_debug_trace_fwd(None); L.gsr_debug_trace_bwd(None); L.gsr_debug_trace_emit(None)
+        np.save(os.path.join(REPO, "gpurun_out", f"trace_bwd_cam{ci}.npy"), bbuf.cpu().numpy()[: 4 * T])
         report[ci] = {"emit": analyse_emit(ebuf.cpu().numpy(), f"cam{ci} emit"),
                       "fwd": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd"),
                       "bwd": analyse(bbuf.cpu().numpy(), T, f"cam{ci} bwd")}
