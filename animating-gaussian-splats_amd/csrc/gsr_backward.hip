@@ -251,6 +251,14 @@ __global__ __launch_bounds__(256) void k_render_bwd(
 // Gradient output write: plain store, or (accumulate bit set, gsr_grads.accumulate) add into the
 // caller's existing gradient -- the same single fp32 add autograd's AccumulateGrad would do.
 __device__ inline void gput(float *p, size_t idx, float v, bool acc) { p[idx] = acc ? p[idx] + v : v; }
+// The same with the old value fetched beforehand (old_load): the outputs a Gaussian accumulates into
+// are read in one batch instead of one load -> add -> store round trip per element.
+template <int N>
+__device__ inline void old_load(const float *p, size_t base, bool acc, float (&o)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) o[k] = acc ? p[base + k] : 0.f;
+}
+__device__ inline void gput_old(float *p, size_t idx, float v, bool acc, float old) { p[idx] = acc ? old + v : v; }
 
 // ------------------------------------------------------------------------------------------
 __device__ inline float3 dnormvdv(float3 v, float3 dv) {
@@ -390,7 +398,7 @@ __device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict
                                         const float4 *__restrict__ part, float4 *stage,
                                         float (&acc)[kPartial]) {
     const int lane = threadIdx.x & 63;
-    const uint32_t e0 = goff[i < P ? i : P], e1 = i < P ? goff[i + 1] : e0;
+    const uint32_t e0 = goff[min(i, P)], e1 = goff[min(i + 1, P)];  // both in flight at once
     const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0);
     const uint32_t E1 = __builtin_amdgcn_readlane(e1, 63);
 #pragma unroll
@@ -404,8 +412,8 @@ __device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict
         for (int t = 0; t < NF4 / 64; ++t)  // clamped index: every load in bounds, none predicated
             v[t] = src[min(lane + 64u * t, n3 - 1u)];
 #pragma unroll
-        for (int t = 0; t < NF4 / 64; ++t)
-            if (lane + 64u * t < n3) stage[lane + 64 * t] = v[t];
+        for (int t = 0; t < NF4 / 64; ++t)  // unpredicated (slots past n3 get a copy, never read):
+            stage[lane + 64 * t] = v[t];     // a predicated store would sink its load into the branch
         wave_lds_sync();
         const uint32_t a = max(e0, cb), b = min(e1, cb + C);
         for (uint32_t e = a; e < b; ++e) {
@@ -459,15 +467,25 @@ __device__ inline void gauss_bwd_one(
         }
         return;
     }
-    gput(dL_dmeans2D, 3 * i, acc[0], a2); gput(dL_dmeans2D, 3 * i + 1, acc[1], a2); gput(dL_dmeans2D, 3 * i + 2, 0.f, a2);
-    // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
-    if (act & GSR_ACT_SIGMOID_OPACITY) {
-        const float o = rec[(size_t)kRecF4 * i + 1].y;
-        gput(dL_dopacity, i, acc[5] * ((1.f - o) * o), ao);
-    } else {
-        gput(dL_dopacity, i, acc[5], ao);
+    {   // screen-space outputs: old values (accumulation) fetched together
+        float o2[3], oo[1], oc[3];
+        old_load(dL_dmeans2D, 3 * (size_t)i, a2, o2);
+        old_load(dL_dopacity, (size_t)i, ao, oo);
+        old_load(dL_dcolors, 3 * (size_t)i, dL_dcolors && ac, oc);
+        gput_old(dL_dmeans2D, 3 * i, acc[0], a2, o2[0]); gput_old(dL_dmeans2D, 3 * i + 1, acc[1], a2, o2[1]);
+        gput_old(dL_dmeans2D, 3 * i + 2, 0.f, a2, o2[2]);
+        // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
+        if (act & GSR_ACT_SIGMOID_OPACITY) {
+            const float o = rec[(size_t)kRecF4 * i + 1].y;
+            gput_old(dL_dopacity, i, acc[5] * ((1.f - o) * o), ao, oo[0]);
+        } else {
+            gput_old(dL_dopacity, i, acc[5], ao, oo[0]);
+        }
+        if (dL_dcolors) {
+            gput_old(dL_dcolors, 3 * i, acc[6], ac, oc[0]); gput_old(dL_dcolors, 3 * i + 1, acc[7], ac, oc[1]);
+            gput_old(dL_dcolors, 3 * i + 2, acc[8], ac, oc[2]);
+        }
     }
-    if (dL_dcolors) { gput(dL_dcolors, 3 * i, acc[6], ac); gput(dL_dcolors, 3 * i + 1, acc[7], ac); gput(dL_dcolors, 3 * i + 2, acc[8], ac); }
     const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
 
     float vm[16], pj[16];
@@ -582,14 +600,26 @@ __device__ inline void gauss_bwd_one(
     } else if (dL_dsh) {
         if (!ash) for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
     }
-    gput(dL_dmeans3D, 3 * i, dm0, a3); gput(dL_dmeans3D, 3 * i + 1, dm1, a3); gput(dL_dmeans3D, 3 * i + 2, dm2, a3);
-    if (scales && !cov3D_precomp) {
+    const bool has_sr = scales && !cov3D_precomp;
+    float o3[3], os[3], orr[4];  // old values of the remaining accumulated outputs, fetched together
+    old_load(dL_dmeans3D, 3 * (size_t)i, a3, o3);
+    old_load(dL_dscales, 3 * (size_t)i, has_sr && dL_dscales && asc, os);
+    old_load(dL_drot, 4 * (size_t)i, has_sr && dL_drot && ar, orr);
+    gput_old(dL_dmeans3D, 3 * i, dm0, a3, o3[0]); gput_old(dL_dmeans3D, 3 * i + 1, dm1, a3, o3[1]);
+    gput_old(dL_dmeans3D, 3 * i + 2, dm2, a3, o3[2]);
+    if (has_sr) {
         float3 ds; float4 dr;
         cov3d_backward(s3, scale_modifier, q, dcov, ds, dr);
         if (act & GSR_ACT_EXP_SCALES) { ds.x *= s3.x; ds.y *= s3.y; ds.z *= s3.z; }
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) dr = act_normalize_bwd(q, qn, dr);
-        if (dL_dscales) { gput(dL_dscales, 3 * i, ds.x, asc); gput(dL_dscales, 3 * i + 1, ds.y, asc); gput(dL_dscales, 3 * i + 2, ds.z, asc); }
-        if (dL_drot) { gput(dL_drot, 4 * i, dr.x, ar); gput(dL_drot, 4 * i + 1, dr.y, ar); gput(dL_drot, 4 * i + 2, dr.z, ar); gput(dL_drot, 4 * i + 3, dr.w, ar); }
+        if (dL_dscales) {
+            gput_old(dL_dscales, 3 * i, ds.x, asc, os[0]); gput_old(dL_dscales, 3 * i + 1, ds.y, asc, os[1]);
+            gput_old(dL_dscales, 3 * i + 2, ds.z, asc, os[2]);
+        }
+        if (dL_drot) {
+            gput_old(dL_drot, 4 * i, dr.x, ar, orr[0]); gput_old(dL_drot, 4 * i + 1, dr.y, ar, orr[1]);
+            gput_old(dL_drot, 4 * i + 2, dr.z, ar, orr[2]); gput_old(dL_drot, 4 * i + 3, dr.w, ar, orr[3]);
+        }
     } else {
         if (dL_dscales && !asc) { dL_dscales[3 * i] = 0.f; dL_dscales[3 * i + 1] = 0.f; dL_dscales[3 * i + 2] = 0.f; }
         if (dL_drot && !ar) { dL_drot[4 * i] = 0.f; dL_drot[4 * i + 1] = 0.f; dL_drot[4 * i + 2] = 0.f; dL_drot[4 * i + 3] = 0.f; }

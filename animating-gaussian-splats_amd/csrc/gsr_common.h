@@ -179,7 +179,19 @@ __device__ inline void sh_rows_from_lds(const float *s, int nrow, float *__restr
     if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         const int n4 = n >> 2;
         float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int q = threadIdx.x; q < n4; q += kShBlock) {
+        constexpr int IT = (kShBlock * RL / 4 + kShBlock - 1) / kShBlock;
+        float4 o[IT];  // ACC: every old float4 of this thread loaded before the first store
+        if (ACC) {
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int q = threadIdx.x + it * kShBlock;
+                o[it] = d4[q < n4 ? q : 0];  // clamped (n4 >= 1 whenever a row exists), unpredicated
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int q = threadIdx.x + it * kShBlock;
+            if (q >= n4) break;
             float f[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -187,10 +199,7 @@ __device__ inline void sh_rows_from_lds(const float *s, int nrow, float *__restr
                 f[j] = s[r * RS + (e - r * RL)];
             }
             float4 v = make_float4(f[0], f[1], f[2], f[3]);
-            if (ACC) {
-                const float4 o = d4[q];
-                v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
-            }
+            if (ACC) v = make_float4(o[it].x + v.x, o[it].y + v.y, o[it].z + v.z, o[it].w + v.w);
             d4[q] = v;
         }
         for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += kShBlock) {
