@@ -35,14 +35,34 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
-# rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh), corrected
-# per MI355X_MICROARCH.md (2 x FETCH_SIZE + WRITE_SIZE): HBM bytes per launch of each kernel
+# rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh): HBM bytes per
+# launch of each kernel, converted per access shape (calibrated_traffic; MI355X_MICROARCH.md's 2 x
+# FETCH_SIZE + WRITE_SIZE is the streaming case and is reported beside it)
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_hbm_pmc.json")
 # SQ counters of the same command (tools/profile_round.sh sq passes): VALU activity per launch
 SQ_SUMMARY = os.path.join(REPO, "profiles", "r01_sq_pmc.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
 PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "render_bwd",
           "gauss_bwd"]
+
+
+def streamed_read_bytes(phase, P, K, N, T):
+    """Lane-contiguous (streaming) reads of one launch; the rest of a render kernel's reads are 64-B
+    record gathers.  profiles/r01_fetch_calib.txt: FETCH_SIZE bills streamed reads at half their bytes
+    and a record gather at one whole 64-B unit, so HBM reads = FETCH_SIZE + streamed / 2."""
+    if phase == "render_bwd":      # point list + slot map per pair; T, n_contrib, dL/dpix per pixel
+        return K * 8 + N * 20 + T * 28
+    if phase == "render_fwd":      # 16-B binning record per pair; order + range per tile
+        return K * 16 + T * 12
+    return None                    # streaming kernels: the guide's x2 applies to the whole FETCH_SIZE
+
+
+def calibrated_traffic(pm, phase, P, K, N, T):
+    """HBM bytes of one launch from the kernel's FETCH_SIZE / WRITE_SIZE (KiB averages)."""
+    f = pm["FETCH_SIZE_KiB_avg"] * 1024
+    w = pm["WRITE_SIZE_KiB_avg"] * 1024
+    s = streamed_read_bytes(phase, P, K, N, T)
+    return int((f + s / 2 if s is not None and s / 2 <= f else 2 * f) + w)
 
 
 def algorithmic_bytes(phase, P, K, N, T, F, sh):
@@ -551,11 +571,13 @@ def main():
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
     F = 12 * (cfg.sh_degree + 1) ** 2 if cfg.sh_degree >= 0 else 12
     avg_ms = tot_ms / max(cnt, 1)
-    traffic = None
+    traffic = traffic_2x = None
     if os.path.exists(PMC_SUMMARY):
         pm = json.load(open(PMC_SUMMARY)).get("k_" + dom)
         if pm:
-            traffic = int(pm["hbm_bytes_per_launch_corrected"])
+            traffic_2x = int(pm["hbm_bytes_per_launch_corrected"])
+            traffic = calibrated_traffic(pm, dom, cfg.P, K, cfg.width * cfg.height,
+                                         ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16))
     valu = None
     if os.path.exists(SQ_SUMMARY):
         q = json.load(open(SQ_SUMMARY)).get("k_" + dom)
@@ -597,6 +619,8 @@ def main():
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
                          "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if traffic else None,
+                         "traffic_2x_fetch": traffic_2x,
+                         "traffic_calibration": "profiles/r01_fetch_calib.txt",
                          "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch),
                          "valu": valu},
             "phase_ms_per_launch": {ph: round(probe[ph][0] / max(probe[ph][1], 1), 5) for ph in PHASES},
