@@ -145,6 +145,11 @@ void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
     a.means3D = g->means3D; a.scales = g->scales; a.rotations = g->rotations; a.opacities = g->opacities;
     a.shs = g->shs; a.colors_precomp = g->colors_precomp; a.cov3D_precomp = g->cov3D_precomp;
     a.viewmatrix = cam->viewmatrix; a.projmatrix = cam->projmatrix; a.campos = cam->campos; a.bg = cam->bg;
+    const bool vz = !cam->viewmatrix_stride[0] && !cam->viewmatrix_stride[1];
+    const bool pz = !cam->projmatrix_stride[0] && !cam->projmatrix_stride[1];
+    a.cs.v0 = vz ? 4 : cam->viewmatrix_stride[0]; a.cs.v1 = vz ? 1 : cam->viewmatrix_stride[1];
+    a.cs.p0 = pz ? 4 : cam->projmatrix_stride[0]; a.cs.p1 = pz ? 1 : cam->projmatrix_stride[1];
+    a.cs.c0 = cam->campos_stride ? cam->campos_stride : 1;
 }
 
 void carve_geom(FwdArgs &a, char *base) {
@@ -288,7 +293,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.focal_x = f.focal_x; a.focal_y = f.focal_y;
     a.means3D = f.means3D; a.scales = f.scales; a.rotations = f.rotations; a.shs = f.shs;
     a.colors_precomp = f.colors_precomp; a.cov3D_precomp = f.cov3D_precomp;
-    a.viewmatrix = f.viewmatrix; a.projmatrix = f.projmatrix; a.campos = f.campos; a.bg = f.bg;
+    a.viewmatrix = f.viewmatrix; a.projmatrix = f.projmatrix; a.campos = f.campos; a.bg = f.bg; a.cs = f.cs;
     a.radii = radii;
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff;
     a.ranges = f.ranges; a.final_T = f.final_T; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;

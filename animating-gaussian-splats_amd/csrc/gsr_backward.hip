@@ -273,9 +273,9 @@ __device__ inline float3 dnormvdv(float3 v, float3 dv) {
 // `dL_dsh` may alias (the same LDS row): phase 1 reads the coefficients (direction derivative),
 // phase 2 writes the coefficient gradients, which depend only on the direction and dL/dRGB.
 template <typename ShPtr, typename OutPtr>
-__device__ inline float3 sh_backward(int deg, int M, float3 mean, const float *campos, ShPtr sh,
+__device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos, ShPtr sh,
                                      const bool *clamped, float3 dL_dcolor, OutPtr dL_dsh, bool acc = false) {
-    const float3 d0 = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
+    const float3 d0 = make_float3(mean.x - campos.x, mean.y - campos.y, mean.z - campos.z);
     const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
     const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
     const float dRGB[3] = {dL_dcolor.x * (clamped[0] ? 0.f : 1.f), dL_dcolor.y * (clamped[1] ? 0.f : 1.f),
@@ -432,7 +432,7 @@ __device__ inline void gauss_bwd_one(
     float h_x, float h_y, const float *__restrict__ means3D, const float *__restrict__ scales,
     const float *__restrict__ rotations, const float *__restrict__ shs,
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
-    const float *__restrict__ projmatrix, const float *__restrict__ campos,
+    const float *__restrict__ projmatrix, const float *__restrict__ campos, CamStrides cs,
     const int *__restrict__ radii, const float (&acc)[kPartial], float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
@@ -489,8 +489,8 @@ __device__ inline void gauss_bwd_one(
     const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
 
     float vm[16], pj[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { vm[k] = viewmatrix[k]; pj[k] = projmatrix[k]; }
+    load_mat16(viewmatrix, cs.v0, cs.v1, vm);
+    load_mat16(projmatrix, cs.p0, cs.p1, pj);
     const float3 mean = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
     float c3[6];
     float3 s3 = make_float3(0, 0, 0);
@@ -587,14 +587,16 @@ __device__ inline void gauss_bwd_one(
     dm2 += (pj[8] * m_w - pj[11] * mul1) * g2x + (pj[9] * m_w - pj[11] * mul2) * g2y;
     if (MC > 0) {
         bool cl[3];
-        (void)sh_to_rgb(D, mean, campos, s_row, cl);  // recompute the forward's clamp mask
-        const float3 d = sh_backward(D, MC, mean, campos, s_row, cl, make_float3(acc[6], acc[7], acc[8]), s_row);
+        const float3 cp = load_campos(campos, cs.c0);
+        (void)sh_to_rgb(D, mean, cp, s_row, cl);  // recompute the forward's clamp mask
+        const float3 d = sh_backward(D, MC, mean, cp, s_row, cl, make_float3(acc[6], acc[7], acc[8]), s_row);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
     } else if (shs) {
         const float *sh = shs + (size_t)i * M * 3;
         bool cl[3];
-        (void)sh_to_rgb(D, mean, campos, sh, cl);
-        const float3 d = sh_backward(D, M, mean, campos, sh, cl, make_float3(acc[6], acc[7], acc[8]),
+        const float3 cp = load_campos(campos, cs.c0);
+        (void)sh_to_rgb(D, mean, cp, sh, cl);
+        const float3 d = sh_backward(D, M, mean, cp, sh, cl, make_float3(acc[6], acc[7], acc[8]),
                                      dL_dsh + (size_t)i * M * 3, ash);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
     } else if (dL_dsh) {
@@ -632,7 +634,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     float h_x, float h_y, const float *__restrict__ means3D, const float *__restrict__ scales,
     const float *__restrict__ rotations, const float *__restrict__ shs,
     const float *__restrict__ cov3D_precomp, const float *__restrict__ viewmatrix,
-    const float *__restrict__ projmatrix, const float *__restrict__ campos,
+    const float *__restrict__ projmatrix, const float *__restrict__ campos, CamStrides cs,
     const int *__restrict__ radii, const uint32_t *__restrict__ goff,
     const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
@@ -652,7 +654,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
         __syncthreads();
     }
     if (i < P) gauss_bwd_one<MC>(i, D, M, W, H, scale_modifier, tan_fovx, tan_fovy, h_x, h_y, means3D,
-                                 scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos,
+                                 scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos, cs,
                                  radii, acc, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
                                  act, rec, accm);
@@ -695,7 +697,7 @@ static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
                                     sizeof(float4) * kRecStageF4<MC> * (kShBlock / 64));
     k_gauss_bwd<MC><<<div_up(a.P, kShBlock), kShBlock, lds, s>>>(
         a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
-        a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos,
+        a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.cs,
         a.radii, a.goff, a.part, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
         a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot, a.act, a.rec, a.accm);
 }

@@ -325,10 +325,21 @@ __device__ inline float3 cov2d(float3 mean, float fx, float fy, float tfx, float
     return make_float3(GM(cov, 0, 0) + 0.3f, GM(cov, 0, 1), GM(cov, 1, 1) + 0.3f);
 }
 
+// Element strides of the camera inputs (gsr_camera, ABI 8): matrix element k (column-major m[k] of
+// the kernels) sits at (k / 4) * m0 + (k % 4) * m1; campos component c at c * c0.
+struct CamStrides { int v0, v1, p0, p1, c0; };
+__device__ inline void load_mat16(const float *__restrict__ m, int s0, int s1, float (&out)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) out[k] = m[(k >> 2) * s0 + (k & 3) * s1];
+}
+__device__ inline float3 load_campos(const float *__restrict__ c, int s) {
+    return c ? make_float3(c[0], c[s], c[2 * s]) : make_float3(0.f, 0.f, 0.f);
+}
+
 // SH -> RGB for one channel set; `sh` points at the Gaussian's (M,3) coefficients (global or LDS).
 template <typename ShPtr>
-__device__ inline float3 sh_to_rgb(int deg, float3 mean, const float *campos, ShPtr sh, bool *clamped) {
-    float3 dir = make_float3(mean.x - campos[0], mean.y - campos[1], mean.z - campos[2]);
+__device__ inline float3 sh_to_rgb(int deg, float3 mean, float3 campos, ShPtr sh, bool *clamped) {
+    float3 dir = make_float3(mean.x - campos.x, mean.y - campos.y, mean.z - campos.z);
     const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
     dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
     float out[3];

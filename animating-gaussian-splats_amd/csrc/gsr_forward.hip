@@ -43,11 +43,14 @@ __global__ __launch_bounds__(256) void k_preprocess(
     const float *__restrict__ projmatrix, const float *__restrict__ campos, int W, int H,
     float tan_fovx, float tan_fovy, float focal_x, float focal_y, int gx, int gy,
     int *__restrict__ radii, float *__restrict__ depth_out, float4 *__restrict__ rec_out,
-    uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out, int act) {
+    uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out, int act, CamStrides cs,
+    uint32_t *__restrict__ tile_count, int T) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
     const int i = i0 + threadIdx.x;
+    // k_bin_count's tile histogram starts from zero: cleared here instead of by a memset launch
+    for (int t = i; t < T; t += (int)gridDim.x * kShBlock) tile_count[t] = 0;
     // this Gaussian's own inputs are loaded first (clamped index for the tail lanes), so their
     // latency overlaps the SH row copy instead of following its barrier
     const int ic = min(i, P - 1);
@@ -66,8 +69,8 @@ __global__ __launch_bounds__(256) void k_preprocess(
     if (i >= P) return;
     // matrices are tiny and uniform: every lane reads the same words (scalar loads)
     float vm[16], pm[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) { vm[k] = viewmatrix[k]; pm[k] = projmatrix[k]; }
+    load_mat16(viewmatrix, cs.v0, cs.v1, vm);
+    load_mat16(projmatrix, cs.p0, cs.p1, pm);
     radii[i] = 0;
     tiles_out[i] = 0;
     rect_out[i] = make_uint2(0, 0);
@@ -104,8 +107,9 @@ __global__ __launch_bounds__(256) void k_preprocess(
         rgb = make_float3(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2]);
     } else {
         bool cl[3];
-        if (MC > 0) rgb = sh_to_rgb(D, p, campos, s_sh + threadIdx.x * RS, cl);
-        else rgb = sh_to_rgb(D, p, campos, shs + (size_t)i * M * 3, cl);
+        const float3 cp = load_campos(campos, cs.c0);
+        if (MC > 0) rgb = sh_to_rgb(D, p, cp, s_sh + threadIdx.x * RS, cl);
+        else rgb = sh_to_rgb(D, p, cp, shs + (size_t)i * M * 3, cl);
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
@@ -650,7 +654,8 @@ static void preprocess_mc(const FwdArgs &a, hipStream_t s) {
     k_preprocess<MC><<<div_up(a.P, kShBlock), kShBlock, sizeof(float) * kShBlock * (MC ? sh_row_stride(MC) : 0), s>>>(
         a.P, a.D, a.M, a.means3D, a.scales, a.scale_modifier, a.rotations, a.opacities, a.shs,
         a.colors_precomp, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
-        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles, a.act);
+        a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles, a.act, a.cs,
+        a.tile_count, a.gx * a.gy);
 }
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {
@@ -669,9 +674,7 @@ hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {
 hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     const BinGrid bg(a.P);
     const int T = a.gx * a.gy;
-    hipError_t e = hipMemsetAsync(a.tile_count, 0, sizeof(uint32_t) * T, s);
-    if (e != hipSuccess) return e;
-    if (bg.NB == 0) return hipSuccess;
+    if (bg.NB == 0) return hipSuccess;  // (tile_count was zeroed by k_preprocess)
     if (T <= kMaxLdsTiles)
         k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
     else

@@ -15,6 +15,7 @@ struct FwdArgs {
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *means3D, *scales, *rotations, *opacities, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;
+    CamStrides cs;
     // geom
     float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff;
     // image
@@ -32,6 +33,7 @@ struct BwdArgs {
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *means3D, *scales, *rotations, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;
+    CamStrides cs;
     const int *radii;
     // saved state
     const float4 *rec; const uint2 *rect;

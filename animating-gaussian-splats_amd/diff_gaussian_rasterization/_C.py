@@ -40,7 +40,8 @@ class _Camera(ctypes.Structure):
                 ("tan_fovx", ctypes.c_float), ("tan_fovy", ctypes.c_float),
                 ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
                 ("campos", ctypes.c_void_p), ("bg", ctypes.c_void_p),
-                ("prefiltered", ctypes.c_int)]
+                ("prefiltered", ctypes.c_int), ("viewmatrix_stride", ctypes.c_int * 2),
+                ("projmatrix_stride", ctypes.c_int * 2), ("campos_stride", ctypes.c_int)]
 
 
 class _Gaussians(ctypes.Structure):
@@ -110,7 +111,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 7  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 8  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -159,15 +160,35 @@ def _stream_ptr(device):
 
 def _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, campos, bg,
             prefiltered, keep):
-    vm, pm = viewmatrix.contiguous().float(), projmatrix.contiguous().float()
+    # the matrices and campos go in as they are (strided views included: the reference's viewmatrix
+    # is a transposed view, campos a column slice) -- no per-call device copy
+    vm, vs = _mat16(viewmatrix)
+    pm, ps = _mat16(projmatrix)
     bg_ = bg.contiguous().float()
-    cp = campos.contiguous().float() if campos is not None and campos.numel() else None
+    cp, cs = None, 0
+    if campos is not None and campos.numel():
+        cp = campos if campos.dtype == torch.float32 and campos.dim() == 1 else campos.reshape(-1).float()
+        cs = cp.stride(0)
     keep += [vm, pm, bg_, cp]
-    if vm.numel() != 16 or pm.numel() != 16:
+    cam = _Camera(int(image_width), int(image_height), float(tan_fovx), float(tan_fovy),
+                  _ptr(vm), _ptr(pm), _ptr(cp) if cp is not None else None,
+                  _ptr(bg_), int(bool(prefiltered)))
+    cam.viewmatrix_stride[0], cam.viewmatrix_stride[1] = vs
+    cam.projmatrix_stride[0], cam.projmatrix_stride[1] = ps
+    cam.campos_stride = cs
+    return cam
+
+
+def _mat16(m):
+    """A 4x4 camera matrix ((4, 4) or (1, 4, 4), any strides) as (fp32 tensor, (row, col) strides)."""
+    if m.numel() != 16:
         raise RuntimeError("viewmatrix/projmatrix must hold 16 floats")
-    return _Camera(int(image_width), int(image_height), float(tan_fovx), float(tan_fovy),
-                   _ptr(vm), _ptr(pm), _ptr(cp) if cp is not None else None,
-                   _ptr(bg_), int(bool(prefiltered)))
+    if m.dtype != torch.float32:
+        m = m.float()
+    m2 = m.reshape(4, 4) if m.dim() != 3 else m[0]
+    if m2.dim() != 2 or m2.shape != (4, 4):
+        raise RuntimeError("viewmatrix/projmatrix must hold 16 floats")
+    return m2, (m2.stride(0), m2.stride(1))
 
 
 def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier, cov3D, keep,

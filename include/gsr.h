@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 7
+#define GSR_ABI_VERSION 8
 
 enum gsr_status {
     GSR_OK = 0,
@@ -63,6 +63,14 @@ typedef struct gsr_camera {
     const float *campos;     /* device, 3 floats */
     const float *bg;         /* device, 3 floats */
     int prefiltered;         /* accepted; the near-plane cull is applied either way */
+    /* ABI >= 8: element strides of the matrices' (row, column) and of campos, so the reference's
+     * views pass as they are -- its viewmatrix is the non-contiguous transpose w2c^T (shared.py:80)
+     * and campos a column slice of inv(w2c) (shared.py:79).  Element k of the 16 read as m[k] (the
+     * column-major convention above) is at (k / 4) * stride[0] + (k % 4) * stride[1].  Zeros mean
+     * contiguous: {4, 1} and 1. */
+    int viewmatrix_stride[2];
+    int projmatrix_stride[2];
+    int campos_stride;
 } gsr_camera;
 
 /* Fused parameter activations (bit mask, gsr_gaussians.activations).  The reference's caller

@@ -329,3 +329,33 @@ def test_fused_parameters_parity(case, cuda):
     for k in ("opacity_logits", "log_scales", "rotation_quaternions"):
         assert gp[k].grad.shape == raw[k].shape
         _close("fused." + k, _np(gp[k].grad), raw[k].grad.numpy(), max_bad_frac=1e-3)
+
+
+def test_strided_camera_inputs_match_contiguous(cuda):
+    """The reference hands the rasterizer a transposed viewmatrix view (shared.py:80) and a column
+    slice of inv(w2c) as campos (shared.py:79); they are read in place through their strides
+    (gsr_camera ABI 8), with results bitwise equal to contiguous copies of the same values."""
+    P = 4_000
+    p = S.synthetic_cloud(P, 0.02, sh_degree=3, seed=11, device=cuda)
+    a = S.activated_inputs(p, 3)
+    a.pop("colors_precomp")
+    rs = S.render_settings(192, 144, S.intrinsics(180.0, 192, 144), S.look_at(70, 0.4, 4), device=cuda,
+                           sh_degree=3)
+    # the reference's layouts built on the device: w2c^T as a transposed view, campos as a column
+    vm_t = rs.viewmatrix.transpose(1, 2).contiguous().transpose(1, 2)
+    pm_t = rs.projmatrix.transpose(1, 2).contiguous().transpose(1, 2)
+    cam4 = torch.zeros(4, 4, device=cuda)
+    cam4[:3, 3] = rs.campos
+    rs = rs._replace(viewmatrix=vm_t, projmatrix=pm_t, campos=cam4[:3, 3])
+    assert not rs.viewmatrix.is_contiguous() and rs.campos.stride(0) == 4
+    rc = rs._replace(viewmatrix=rs.viewmatrix.contiguous(), projmatrix=rs.projmatrix.contiguous(),
+                     campos=rs.campos.contiguous())
+    dl = S.upstream_grad(144, 192, device=cuda)
+    outs = []
+    for r in (rs, rc):
+        leaves = {k: v.detach().clone().requires_grad_(True) for k, v in a.items()}
+        img, radii, depth = GaussianRasterizer(raster_settings=r)(**leaves)
+        img.backward(dl)
+        outs.append([img.detach(), radii, depth.detach()] + [leaves[k].grad for k in sorted(leaves)])
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
