@@ -154,6 +154,27 @@ class _Allocator:
         return t.data_ptr()
 
 
+class _device_guard:
+    """Make `dev` the current HIP device for the duration of a libgsr call (the library launches on
+    the current device); free when it already is, which is the common case."""
+
+    def __init__(self, dev):
+        self.idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.prev = None
+
+    def __enter__(self):
+        cur = torch.cuda.current_device()
+        if cur != self.idx:
+            self.prev = cur
+            torch.cuda.set_device(self.idx)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            torch.cuda.set_device(self.prev)
+        return False
+
+
 def _stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -223,9 +244,10 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     radii = torch.empty((P,), dtype=torch.int32, device=dev)  # preprocess writes every entry
     alloc = _Allocator(dev)
     nr = ctypes.c_int(0)
-    _check(L.gsr_forward(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
-                         depth.data_ptr(), radii.data_ptr() if P else None, ctypes.byref(nr),
-                         _stream_ptr(dev)))
+    with _device_guard(dev):  # launches go to dev even when another device is current
+        _check(L.gsr_forward(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
+                             depth.data_ptr(), radii.data_ptr() if P else None, ctypes.byref(nr),
+                             _stream_ptr(dev)))
     b = alloc.buffers
     return nr.value, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
 
@@ -271,9 +293,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     keep.append(dpix)
     grads = _Grads(*[t.data_ptr() if t.numel() else None for t in out], acc_bits)
     alloc = _Allocator(dev)
-    _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
-                          geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
-                          dpix.data_ptr(), None, alloc.cb, None, ctypes.byref(grads), _stream_ptr(dev)))
+    with _device_guard(dev):
+        _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
+                              geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+                              dpix.data_ptr(), None, alloc.cb, None, ctypes.byref(grads), _stream_ptr(dev)))
     return out
 
 
@@ -285,8 +308,9 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         return present
     m = means3D.contiguous().float()
     vm, pm = viewmatrix.contiguous().float(), projmatrix.contiguous().float()
-    _check(L.gsr_mark_visible(P, _ptr(m), _ptr(vm), _ptr(pm), present.data_ptr(),
-                              _stream_ptr(means3D.device)))
+    with _device_guard(means3D.device):
+        _check(L.gsr_mark_visible(P, _ptr(m), _ptr(vm), _ptr(pm), present.data_ptr(),
+                                  _stream_ptr(means3D.device)))
     return present
 
 
