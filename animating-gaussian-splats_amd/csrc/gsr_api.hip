@@ -56,7 +56,9 @@ std::map<std::string, int> g_host_n;
 hipEvent_t ev_get() {
     if (!g_evpool.empty()) { hipEvent_t e = g_evpool.back(); g_evpool.pop_back(); return e; }
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    // timing only: no system-scope fence (its L2 writeback + invalidate would also slow the kernel
+    // that follows the event, and the host reads the events after a stream synchronisation anyway)
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -309,6 +311,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
     const ScratchLayout SL(num_rendered);
     a.part = (float4 *)(scr + SL.part);
+    { Phase ph(s, "tile_order_bwd"); HIP_TRY(launch_tile_order_bwd(a, s)); }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
     { Phase ph(s, "gauss_bwd"); HIP_TRY(launch_gauss_bwd(a, s)); }
     return GSR_OK;

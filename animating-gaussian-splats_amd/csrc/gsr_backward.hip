@@ -680,12 +680,15 @@ static int device_simds() {
     return cache[dev];
 }
 
+hipError_t launch_tile_order_bwd(const BwdArgs &a, hipStream_t s) {
+    if (a.K == 0) return hipSuccess;
+    k_tile_order_bwd<<<1, 1024, 0, s>>>(a.gx * a.gy, a.tile_maxc, a.tile_order_b, device_simds());
+    return hipGetLastError();
+}
+
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (a.K == 0) return hipSuccess;
-    k_tile_order_bwd<<<1, 1024, 0, s>>>(T, a.tile_maxc, a.tile_order_b, device_simds());
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     k_render_bwd<<<div_up(T, kTilesPerBlock), 64 * kTilesPerBlock, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_b, a.ranges, a.point_list, a.rec, a.bg, a.final_T,
                                   a.n_contrib, a.tile_maxc, a.slot_emit, a.dL_dcolor, a.part);
     return hipGetLastError();

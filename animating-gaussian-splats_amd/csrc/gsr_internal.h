@@ -60,6 +60,7 @@ hipError_t launch_zero(float *p, size_t n, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 
+hipError_t launch_tile_order_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 
