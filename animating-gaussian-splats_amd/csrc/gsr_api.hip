@@ -79,6 +79,42 @@ struct Phase {
     }
 };
 
+// Cross-stream order of the gradient writes.  A caller may render its views on several HIP streams
+// (bench.py --streams, splat_train) so one view's memory-bound k_gauss_bwd overlaps another view's
+// VALU-bound render kernels; the views' gradients still land in the same buffers, so every
+// k_gauss_bwd waits for the previous one that wrote the same output set (keyed by dL_dmeans3D) when
+// that one ran on another stream.  Additions then happen in call order: the result is bitwise the
+// single-stream one.  Same-stream calls add nothing (stream order already holds).
+struct GradWriter { const void *key = nullptr; hipStream_t s = nullptr; hipEvent_t ev = nullptr; };
+std::mutex g_gw_mu;
+GradWriter g_gw[16];
+int g_gw_next = 0;
+
+template <typename Launch>
+hipError_t ordered_grad_write(const void *key, hipStream_t s, Launch launch) {
+    std::lock_guard<std::mutex> lk(g_gw_mu);
+    GradWriter *w = nullptr;
+    for (auto &e : g_gw)
+        if (e.key == key) { w = &e; break; }
+    if (w && w->s != s) {
+        const hipError_t e = hipStreamWaitEvent(s, w->ev, 0);
+        if (e != hipSuccess) return e;
+    }
+    if (!w) {
+        w = &g_gw[g_gw_next];
+        g_gw_next = (g_gw_next + 1) % 16;
+        w->key = key;
+    }
+    if (!w->ev) {
+        const hipError_t e = hipEventCreateWithFlags(&w->ev, hipEventDisableTiming);
+        if (e != hipSuccess) { w->key = nullptr; return e; }
+    }
+    const hipError_t e = launch();
+    if (e != hipSuccess) return e;
+    w->s = s;
+    return hipEventRecord(w->ev, s);
+}
+
 // Host-mapped, coherent pinned word per thread for the num_rendered read-back.  k_bin_scan stores
 // K into it with a system-scope store; the host spins on it (no copy kernel, no runtime wait).
 struct HostWord { uint32_t *h = nullptr; uint32_t *d = nullptr; };
@@ -313,7 +349,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.part = (float4 *)(scr + SL.part);
     { Phase ph(s, "tile_order_bwd"); HIP_TRY(launch_tile_order_bwd(a, s)); }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
-    { Phase ph(s, "gauss_bwd"); HIP_TRY(launch_gauss_bwd(a, s)); }
+    { Phase ph(s, "gauss_bwd"); HIP_TRY(ordered_grad_write(a.dL_dmeans3D, s, [&] { return launch_gauss_bwd(a, s); })); }
     return GSR_OK;
 }
 

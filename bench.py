@@ -395,6 +395,10 @@ def main():
                     help="views rendered per GPU per step (train.py:757 sums the losses of 5 views "
                          "per optimisation step)")
     ap.add_argument("--config", default="C3")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the step's views alternate over: one view's memory-bound "
+                         "per-Gaussian backward overlaps the next view's VALU-bound render kernels; "
+                         "libgsr orders the gradient writes across streams (bitwise the 1-stream result)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path on one GPU)")
@@ -458,10 +462,18 @@ def main():
         return splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)],
                                     rank, world)
 
+    main = torch.cuda.current_stream(dev)
+    streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1) - 1)]
+
     def step(it):
-        for ci in views_of(it):
-            img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
-            img.backward(dl)
+        for s in streams[1:]:
+            s.wait_stream(main)  # the previous step's all-reduce / gradient reset
+        for k, ci in enumerate(views_of(it)):
+            with torch.cuda.stream(streams[k % len(streams)]):
+                img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
+                img.backward(dl)
+        for s in streams[1:]:
+            main.wait_stream(s)
         if reducer is not None:
             reducer.reduce()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
             reducer.zero_()
@@ -614,7 +626,8 @@ def main():
                                    f"{cfg.width}x{cfg.height}, 27-camera rig, {V} view(s)/GPU/step, fwd+bwd",
                        "gaussians": cfg.P, "views_per_gpu_per_step": V,
                        "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
-                       "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}"},
+                       "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}",
+                       "streams_per_gpu": len(streams)},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
