@@ -275,16 +275,19 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     keep_col = not skip_unused or has(colors)
     keep_cov = not skip_unused or has(cov3D_precomp)
     keep_sr = not skip_unused or (has(scales) and has(rotations))
-    out = [e(P, 3), e(P, 3) if keep_col else e(0), e(P, 1), e(P, 3), e(P, 6) if keep_cov else e(0),
-           e(P, M, 3), e(P, 3) if keep_sr else e(0), e(P, 4) if keep_sr else e(0)]
+    shapes = [(P, 3), (P, 3) if keep_col else (0,), (P, 1), (P, 3), (P, 6) if keep_cov else (0,),
+              (P, M, 3), (P, 3) if keep_sr else (0,), (P, 4) if keep_sr else (0,)]
+    acc = list(accumulate_into or ()) + [None] * 8
+    out = []
     acc_bits = 0
-    for k, t in enumerate(accumulate_into or ()):
-        if t is None or out[k].numel() == 0:
+    for k, shp in enumerate(shapes):  # outputs that accumulate into a caller tensor are not allocated
+        t = acc[k]
+        if t is None or shp == (0,):
+            out.append(e(*shp))
             continue
-        if t.shape != out[k].shape or t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
-            raise RuntimeError(f"accumulate_into[{k}]: expected a contiguous float32 {tuple(out[k].shape)} "
-                               f"tensor on {dev}")
-        out[k] = t
+        if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+            raise RuntimeError(f"accumulate_into[{k}]: expected a contiguous float32 {shp} tensor on {dev}")
+        out.append(t)
         acc_bits |= 1 << k
     out = tuple(out)
     if P == 0:

@@ -4,6 +4,7 @@
 # passes of SQ counters (VALU / LDS / SALU activity) for the compute-bound kernels.  Same bench
 # arguments in every pass, so the per-launch averages describe the command bench.py reports on.
 # usage (on the box, from the repo root): bash tools/profile_round.sh <tag> [bench args...]
+# TIMED_RANGE (default 40:140 = bench defaults: (warmup 5 + probe 3) x 5 views .. + 20 steps x 5 views)
 # outputs: gpurun_out/prof_<tag>/{trace,fetch,write,sq1,sq2}/ raw CSV, trace_summary.txt, hbm_pmc.json, sq_pmc.json
 set -u
 tag=${1:-r01}; shift || true
@@ -28,7 +29,7 @@ for pass in 1 2; do
 done
 echo "sq ok"
 cd "$R"
-python3 tools/rocprof_summary.py trace "$O/trace" --last 20 --out "$O/trace_summary.json" > "$O/trace_summary.txt"
+python3 tools/rocprof_summary.py trace "$O/trace" --last 20 --range ${TIMED_RANGE:-40:140} --out "$O/trace_summary.json" > "$O/trace_summary.txt"
 python3 tools/rocprof_summary.py pmc "$O/fetch" "$O/write" --out "$O/hbm_pmc.json" > "$O/hbm_pmc.txt"
 python3 tools/rocprof_summary.py sq "$O/sq1" "$O/sq2" --out "$O/sq_pmc.json" > "$O/sq_pmc.txt"
 cp "$O"/trace/*/*_kernel_stats.csv "$O/kernel_stats.csv" 2>/dev/null || true

@@ -1,8 +1,9 @@
 """Summarise rocprofv3 CSV output into per-kernel tables (profiles/ evidence for bench.py).
 
 Usage:
-  python tools/rocprof_summary.py trace  <dir> [--last N] [--out x.json]
-        -> per-kernel calls / avg / total us (+ average of the last N launches = bench's timed steps)
+  python tools/rocprof_summary.py trace  <dir> [--last N] [--range A:B] [--out x.json]
+        -> per-kernel calls / avg / total us (+ average of the last N launches; + average of launches
+           [A, B) of each once-per-view kernel = bench.py's timed region, (W+probe)V : (W+probe+K)V)
   python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> [--out profiles/x.json]
         -> per-kernel avg FETCH_SIZE / WRITE_SIZE per launch and corrected HBM bytes
   python tools/rocprof_summary.py sq     <dir> [<dir> ...] [--out profiles/x.json]
@@ -36,15 +37,21 @@ def _rows(d, pattern):
             yield from csv.DictReader(fh)
 
 
-def trace(d, last=0):
+def trace(d, last=0, rng=None):
     acc = defaultdict(list)
     rows = sorted(_rows(d, "*kernel_trace.csv"), key=lambda r: int(r["Start_Timestamp"]))
     for r in rows:
         acc[_short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     out = {k: {"calls": len(v), "avg_us": sum(v) / len(v), "total_us": sum(v)} for k, v in acc.items()}
-    if last:  # launches of bench.py's timed region (the last `last` calls of a once-per-step kernel)
+    if last:  # the last `last` calls of each kernel
         for k, v in acc.items():
-            out[k]["timed_avg_us"] = sum(v[-last:]) / len(v[-last:])
+            out[k]["last_avg_us"] = sum(v[-last:]) / len(v[-last:])
+    if rng:  # launches [a, b) of each once-per-view kernel: bench.py's timed region
+        a, b = rng
+        for k, v in acc.items():
+            if len(v) >= b:
+                out[k]["timed_avg_us"] = sum(v[a:b]) / (b - a)
+                out[k]["timed_launches"] = [a, b]
     return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_us"]))
 
 
@@ -89,11 +96,14 @@ def main():
     mode = sys.argv[1]
     if mode == "trace":
         last = int(sys.argv[sys.argv.index("--last") + 1]) if "--last" in sys.argv else 0
-        t = trace(sys.argv[2], last)
-        print(f"{'kernel':<28}{'calls':>8}{'avg_us':>12}{'total_us':>14}" + (f"{'last%d_avg_us' % last:>16}" if last else ""))
+        rng = tuple(int(x) for x in sys.argv[sys.argv.index("--range") + 1].split(":")) if "--range" in sys.argv else None
+        t = trace(sys.argv[2], last, rng)
+        print(f"{'kernel':<28}{'calls':>8}{'avg_us':>12}{'total_us':>14}" + (f"{'last%d_avg_us' % last:>16}" if last else "")
+              + (f"{'timed_avg_us':>14}" if rng else ""))
         for k, v in t.items():
             print(f"{k:<28}{v['calls']:>8}{v['avg_us']:>12.2f}{v['total_us']:>14.1f}"
-                  + (f"{v['timed_avg_us']:>16.2f}" if last else ""))
+                  + (f"{v['last_avg_us']:>16.2f}" if last else "")
+                  + (f"{v['timed_avg_us']:>14.2f}" if rng and 'timed_avg_us' in v else ""))
         if "--out" in sys.argv:
             json.dump(t, open(sys.argv[sys.argv.index("--out") + 1], "w"), indent=1)
     elif mode == "sq":

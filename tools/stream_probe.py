@@ -18,17 +18,23 @@ act.pop("colors_precomp")
 leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
 cams = S.scene_cameras(cfg, device=dev)
 dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
-for nstreams in (1, 2, 1, 2):
+for nstreams, summed in ((1, False), (2, False), (1, True), (2, True), (3, True)):
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nstreams - 1)]
     main = torch.cuda.current_stream()
     def step(it):
         for s in streams[1:]:
             s.wait_stream(main)
+        imgs = []
         for k in range(5):
             ci = (it * 5 + k) % len(cams)
             with torch.cuda.stream(streams[k % nstreams]):
                 img, _, _ = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
-                img.backward(dl)
+                if summed:
+                    imgs.append(img)
+                else:
+                    img.backward(dl)
+        if summed:  # train.py: the summed loss of the step's views, one backward
+            torch.autograd.backward(imgs, [dl] * len(imgs))
         for s in streams[1:]:
             main.wait_stream(s)
         for p in leaves.values():
@@ -41,4 +47,4 @@ for nstreams in (1, 2, 1, 2):
         step(it)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / 20
-    print(f"streams={nstreams} ms/step {dt*1e3:.3f}  Msplats/s {5*cfg.P/dt/1e6:.1f}", flush=True)
+    print(f"streams={nstreams} summed={summed} ms/step {dt*1e3:.3f}  Msplats/s {5*cfg.P/dt/1e6:.1f}", flush=True)
