@@ -290,6 +290,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         out.append(t)
         acc_bits |= 1 << k
     out = tuple(out)
+    if acc_bits:  # the kernel writes caller tensors on this stream: the allocator must not recycle
+        cs = torch.cuda.current_stream(dev)  # them before it is done (views on several streams)
+        for k in range(8):
+            if acc_bits >> k & 1:
+                out[k].record_stream(cs)
     if P == 0:
         return out
     dpix = dL_dout_color.contiguous().float()

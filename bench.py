@@ -395,7 +395,7 @@ def main():
                     help="views rendered per GPU per step (train.py:757 sums the losses of 5 views "
                          "per optimisation step)")
     ap.add_argument("--config", default="C3")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the step's views alternate over: one view's memory-bound "
                          "per-Gaussian backward overlaps the next view's VALU-bound render kernels; "
                          "libgsr orders the gradient writes across streams (bitwise the 1-stream result)")
@@ -466,15 +466,20 @@ def main():
     streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1) - 1)]
 
     def step(it):
-        for s in streams[1:]:
-            s.wait_stream(main)  # the previous step's all-reduce / gradient reset
+        # N > 1: every stream's first gradient write follows the previous step's all-reduce and
+        # reset on the main stream, and the all-reduce follows every stream's last write.  N = 1:
+        # no cross-stream joins at all (they would drain the pipeline at each step boundary): libgsr
+        # orders the gradient writes and record_stream keeps freed gradients from early reuse.
+        if reducer is not None:
+            for s in streams[1:]:
+                s.wait_stream(main)
         for k, ci in enumerate(views_of(it)):
             with torch.cuda.stream(streams[k % len(streams)]):
                 img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
                 img.backward(dl)
-        for s in streams[1:]:
-            main.wait_stream(s)
         if reducer is not None:
+            for s in streams[1:]:
+                main.wait_stream(s)
             reducer.reduce()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
             reducer.zero_()
             leaves["means2D"].grad = None
