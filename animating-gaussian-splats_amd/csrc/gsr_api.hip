@@ -90,6 +90,8 @@ std::mutex g_gw_mu;
 GradWriter g_gw[16];
 int g_gw_next = 0;
 
+hipError_t no_launch() { return hipSuccess; }
+
 template <typename Launch>
 hipError_t ordered_grad_write(const void *key, hipStream_t s, Launch launch) {
     std::lock_guard<std::mutex> lk(g_gw_mu);
@@ -350,6 +352,12 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     { Phase ph(s, "tile_order_bwd"); HIP_TRY(launch_tile_order_bwd(a, s)); }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
     { Phase ph(s, "gauss_bwd"); HIP_TRY(ordered_grad_write(a.dL_dmeans3D, s, [&] { return launch_gauss_bwd(a, s); })); }
+    return GSR_OK;
+}
+
+int gsr_grad_fence(const float *dL_dmeans3D, void *stream) {
+    if (!dL_dmeans3D) return fail(GSR_ERR_ARG, "gsr_grad_fence: null gradient");
+    HIP_TRY(ordered_grad_write(dL_dmeans3D, (hipStream_t)stream, no_launch));
     return GSR_OK;
 }
 

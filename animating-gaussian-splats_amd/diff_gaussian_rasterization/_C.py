@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "gsr_ssim_scratch_bytes", "gsr_l1_ssim_forward", "gsr_l1_ssim_backward",
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
+    "gsr_grad_fence",
 )
 
 
@@ -80,6 +81,8 @@ def load_library():
     L.gsr_backward.restype = i
     L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
                                vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]
+    L.gsr_grad_fence.restype = i
+    L.gsr_grad_fence.argtypes = [vp, vp]
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):
@@ -111,7 +114,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 8  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 9  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -306,6 +309,15 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                               geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
                               dpix.data_ptr(), None, alloc.cb, None, ctypes.byref(grads), _stream_ptr(dev)))
     return out
+
+
+def grad_fence(means3D_grad):
+    """Declare that the work queued so far on the current stream writes the gradient set whose
+    means3D gradient is ``means3D_grad`` (an all-reduce, a reset): the next rasterizer backward
+    into that set, on any stream, is ordered after it (gsr_grad_fence)."""
+    dev = means3D_grad.device
+    with _device_guard(dev):
+        _check(load_library().gsr_grad_fence(means3D_grad.data_ptr(), _stream_ptr(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -463,25 +463,29 @@ def main():
                                     rank, world)
 
     main = torch.cuda.current_stream(dev)
-    streams = [main] + [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1) - 1)]
+    # side streams for the views: the main stream keeps the collectives (N > 1) out of their way
+    streams = [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1))]
+    for s in streams:
+        s.wait_stream(main)  # the setup's parameters, leaves and upstream gradient
+
+    if reducer is not None:  # the bucket's zeroing (main stream) precedes the first backward
+        _C.grad_fence(leaves["means3D"].grad)
 
     def step(it):
-        # N > 1: every stream's first gradient write follows the previous step's all-reduce and
-        # reset on the main stream, and the all-reduce follows every stream's last write.  N = 1:
-        # no cross-stream joins at all (they would drain the pipeline at each step boundary): libgsr
-        # orders the gradient writes and record_stream keeps freed gradients from early reuse.
-        if reducer is not None:
-            for s in streams[1:]:
-                s.wait_stream(main)
+        # No stream waits for another at the step start: libgsr orders the gradient writes across
+        # streams, record_stream keeps freed gradients from early reuse, and for N > 1 the bucket's
+        # all-reduce + reset on the main stream is declared with grad_fence, so the next step's
+        # forwards run during the all-reduce and only its first gradient write waits for it.
         for k, ci in enumerate(views_of(it)):
             with torch.cuda.stream(streams[k % len(streams)]):
                 img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
                 img.backward(dl)
         if reducer is not None:
-            for s in streams[1:]:
+            for s in streams:
                 main.wait_stream(s)
             reducer.reduce()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
             reducer.zero_()
+            _C.grad_fence(leaves["means3D"].grad)
             leaves["means2D"].grad = None
         else:
             for p in leaves.values():

@@ -44,3 +44,35 @@ def test_multistream_views_bitwise_equal(nstreams, cuda):
         assert torch.equal(x, y)
     for k in g1:
         assert torch.equal(g1[k], gn[k]), k
+
+
+def test_grad_fence_orders_a_reset_before_the_next_backward(cuda):
+    """A reset of the gradients on another stream, declared with grad_fence, is ordered before the
+    next backward's accumulation into them (the N > 1 bench: all-reduce + reset on the main stream
+    while the next step's forwards already run on side streams)."""
+    from diff_gaussian_rasterization import _C
+    P, W, H = 200_000, 640, 480
+    p = S.synthetic_cloud(P, 0.01, sh_degree=3, seed=6, device=cuda)
+    a = S.activated_inputs(p, 3)
+    a.pop("colors_precomp")
+    cam = S.render_settings(W, H, S.intrinsics(600.0, W, H), S.look_at(20, 0.3, 4), device=cuda, sh_degree=3)
+    dl = S.upstream_grad(H, W, device=cuda)
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in a.items()}
+    main = torch.cuda.current_stream()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for s in (s1, s2):
+        s.wait_stream(main)
+    with torch.cuda.stream(s1):  # first view: creates the gradients
+        GaussianRasterizer(raster_settings=cam)(**leaves)[0].backward(dl)
+    main.wait_stream(s1)
+    for v in leaves.values():  # the "all-reduce + reset" on the main stream ...
+        v.grad.mul_(3.0).zero_()
+    _C.grad_fence(leaves["means3D"].grad)  # ... declared to the library
+    with torch.cuda.stream(s2):  # second view, other stream: accumulates into the reset gradients
+        GaussianRasterizer(raster_settings=cam)(**leaves)[0].backward(dl)
+    torch.cuda.synchronize()
+    ref = {k: v.detach().clone().requires_grad_(True) for k, v in a.items()}
+    GaussianRasterizer(raster_settings=cam)(**ref)[0].backward(dl)
+    torch.cuda.synchronize()
+    for k in ref:
+        assert torch.equal(leaves[k].grad, ref[k].grad), k
