@@ -120,7 +120,9 @@ struct ScratchLayout {
 
 // SH rows staged through LDS by the per-Gaussian kernels (coalesced global traffic): compile-time
 // coefficient counts for the degrees the reference can activate; other counts use direct loads.
-constexpr int kShBlock = 256;
+// Threads (= Gaussians) per block of the SH-staging kernels (k_preprocess, k_gauss_bwd): 25 KB of
+// LDS at SH3, small enough to co-run with other streams' render kernels (256 was 2 % slower).
+constexpr int kShBlock = 128;
 __host__ __device__ constexpr int sh_row_stride(int MC) { return (3 * MC) | 1; }  // odd: no bank conflicts
 
 // Block copy of `nrow` SH rows (3 MC floats each, contiguous in global memory) into LDS rows of
