@@ -124,6 +124,21 @@ __device__ __forceinline__ void render_bwd_tile(
     // 6..8 sum cs (the first five still to be scaled by the opacity); wave_pair_sums row map:
     const int xslot = (row == 0) ? 0 : (row == 1) ? 4 : (row == 2) ? 1 : 6;
     const int yslot = (row == 0) ? 2 : (row == 1) ? 7 : (row == 2) ? 3 : 8;
+    // the batch ending at `e` (slots [max(e - 64, 0), e)): lane j's slot, its Gaussian's whole render
+    // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
+    // behind the current batch's pairs
+    float4 a_n = make_float4(0.f, 0.f, 0.f, 0.f), b_n = a_n, c_n = a_n, cj_n = a_n;
+    uint32_t em_n = 0;
+    auto fetch = [&](int e) {
+        const int st = e > 64 ? e - 64 : 0;
+        if (lane < e - st) {
+            const uint32_t g = point_list[rg.x + st + lane];
+            em_n = slot_emit[rg.x + st + lane];
+            a_n = rec[(size_t)kRecF4 * g]; b_n = rec[(size_t)kRecF4 * g + 1];
+            c_n = rec[(size_t)kRecF4 * g + 2]; cj_n = rec[(size_t)kRecF4 * g + 3];
+        }
+    };
+    if (maxc > 0) fetch(maxc);
     for (int end = maxc; end > 0; end -= 64) {
         const int start = end > 64 ? end - 64 : 0;
         const int cnt = end - start;
@@ -133,12 +148,11 @@ __device__ __forceinline__ void render_bwd_tile(
         // quarter whose pixels all precede this slot in the forward's order (p >= its max
         // n_contrib) is skipped too
         uint32_t qmask = 0;
-        uint32_t g_st = 0;  // Gaussian this lane staged (its record is re-read for the epilogue)
+        const float4 cj = cj_n;  // exact conic (a, b, c) of the Gaussian this lane stages
+        const uint32_t em = em_n;
         if (lane < cnt) {
             const uint32_t p = (uint32_t)(start + lane);
-            const uint32_t g = point_list[rg.x + p];
-            g_st = g;
-            const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1], c = rec[(size_t)kRecF4 * g + 2];
+            const float4 a = a_n, b = b_n, c = c_n;
             s_a[lane] = a; s_b[lane] = b;
             const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
 #pragma unroll
@@ -148,6 +162,7 @@ __device__ __forceinline__ void render_bwd_tile(
                     qmask |= 1u << k;
             s_c[lane] = make_float4(c.x, c.y, c.z, __uint_as_float(qmask));  // .w: the quarter mask
         }
+        if (end > 64) fetch(end - 64);
         uint64_t m = __ballot(qmask != 0);
         wave_lds_sync();
         while (m) {
@@ -208,8 +223,6 @@ __device__ __forceinline__ void render_bwd_tile(
         }
         wave_lds_sync();
         if (lane < cnt) {
-            const float4 cj = rec[(size_t)kRecF4 * g_st + 3];  // exact conic (a, b, c)
-            const uint32_t em = slot_emit[rg.x + start + lane];
             const float *s2 = s_out + lane * kPartial;
             float sm[kPartial];
 #pragma unroll
