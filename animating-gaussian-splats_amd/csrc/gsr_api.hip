@@ -12,6 +12,8 @@
 #include <cstring>
 #include <chrono>
 #include <map>
+#include <memory>
+#include <unordered_map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -81,40 +83,55 @@ struct Phase {
 
 // Cross-stream order of the gradient writes.  A caller may render its views on several HIP streams
 // (bench.py --streams, splat_train) so one view's memory-bound k_gauss_bwd overlaps another view's
-// VALU-bound render kernels; the views' gradients still land in the same buffers, so every
-// k_gauss_bwd waits for the previous one that wrote the same output set (keyed by dL_dmeans3D) when
-// that one ran on another stream.  Additions then happen in call order: the result is bitwise the
-// single-stream one.  Same-stream calls add nothing (stream order already holds).
-struct GradWriter { const void *key = nullptr; hipStream_t s = nullptr; hipEvent_t ev = nullptr; };
+// VALU-bound render kernels; the views' gradients still land in the same buffers.  Every gradient
+// output pointer a k_gauss_bwd writes is tracked with the stream and event of its last writer; the
+// next write of ANY of those pointers from another stream waits for that event first.  Additions then
+// happen in call order and the result is bitwise the single-stream one.  Same-stream writes add no
+// wait (stream order already holds).  Entries are dropped only once their event has completed (a
+// later writer then has nothing to wait for), so no pending write is ever forgotten, however many
+// gradient sets are in flight.
+struct GradEvent {
+    hipEvent_t ev = nullptr;
+    ~GradEvent() { if (ev) (void)hipEventDestroy(ev); }
+};
+struct GradWriter { hipStream_t s = nullptr; std::shared_ptr<GradEvent> ev; };
 std::mutex g_gw_mu;
-GradWriter g_gw[16];
-int g_gw_next = 0;
+std::unordered_map<const void *, GradWriter> g_gw;
+constexpr size_t kGradPruneAt = 1024;  // scan for completed entries when the table grows past this
 
 hipError_t no_launch() { return hipSuccess; }
 
 template <typename Launch>
-hipError_t ordered_grad_write(const void *key, hipStream_t s, Launch launch) {
+hipError_t ordered_grad_write(const void *const *keys, int nkeys, hipStream_t s, Launch launch) {
     std::lock_guard<std::mutex> lk(g_gw_mu);
-    GradWriter *w = nullptr;
-    for (auto &e : g_gw)
-        if (e.key == key) { w = &e; break; }
-    if (w && w->s != s) {
-        const hipError_t e = hipStreamWaitEvent(s, w->ev, 0);
-        if (e != hipSuccess) return e;
+    const GradEvent *waited[16];
+    int nw = 0;
+    for (int k = 0; k < nkeys; ++k) {
+        if (!keys[k]) continue;
+        auto it = g_gw.find(keys[k]);
+        if (it == g_gw.end() || it->second.s == s) continue;
+        const GradEvent *e = it->second.ev.get();
+        bool seen = false;
+        for (int j = 0; j < nw; ++j) seen = seen || waited[j] == e;
+        if (seen) continue;
+        const hipError_t r = hipStreamWaitEvent(s, e->ev, 0);
+        if (r != hipSuccess) return r;
+        if (nw < 16) waited[nw++] = e;
     }
-    if (!w) {
-        w = &g_gw[g_gw_next];
-        g_gw_next = (g_gw_next + 1) % 16;
-        w->key = key;
+    auto ev = std::make_shared<GradEvent>();
+    hipError_t r = hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming);
+    if (r != hipSuccess) { ev->ev = nullptr; return r; }
+    r = launch();
+    if (r != hipSuccess) return r;
+    r = hipEventRecord(ev->ev, s);
+    if (r != hipSuccess) return r;
+    for (int k = 0; k < nkeys; ++k)
+        if (keys[k]) g_gw[keys[k]] = GradWriter{s, ev};
+    if (g_gw.size() > kGradPruneAt) {
+        for (auto it = g_gw.begin(); it != g_gw.end();)
+            it = hipEventQuery(it->second.ev->ev) == hipSuccess ? g_gw.erase(it) : std::next(it);
     }
-    if (!w->ev) {
-        const hipError_t e = hipEventCreateWithFlags(&w->ev, hipEventDisableTiming);
-        if (e != hipSuccess) { w->key = nullptr; return e; }
-    }
-    const hipError_t e = launch();
-    if (e != hipSuccess) return e;
-    w->s = s;
-    return hipEventRecord(w->ev, s);
+    return hipSuccess;
 }
 
 // Host-mapped, coherent pinned word per thread for the num_rendered read-back.  k_bin_scan stores
@@ -351,13 +368,15 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.part = (float4 *)(scr + SL.part);
     { Phase ph(s, "tile_order_bwd"); HIP_TRY(launch_tile_order_bwd(a, s)); }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
-    { Phase ph(s, "gauss_bwd"); HIP_TRY(ordered_grad_write(a.dL_dmeans3D, s, [&] { return launch_gauss_bwd(a, s); })); }
+    const void *written[8] = {a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity, a.dL_dmeans3D,
+                              a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot};
+    { Phase ph(s, "gauss_bwd"); HIP_TRY(ordered_grad_write(written, 8, s, [&] { return launch_gauss_bwd(a, s); })); }
     return GSR_OK;
 }
 
-int gsr_grad_fence(const float *dL_dmeans3D, void *stream) {
-    if (!dL_dmeans3D) return fail(GSR_ERR_ARG, "gsr_grad_fence: null gradient");
-    HIP_TRY(ordered_grad_write(dL_dmeans3D, (hipStream_t)stream, no_launch));
+int gsr_grad_fence(const void *const *grads, int n, void *stream) {
+    if (n < 0 || (n > 0 && !grads)) return fail(GSR_ERR_ARG, "gsr_grad_fence: bad gradient list");
+    HIP_TRY(ordered_grad_write(grads, n, (hipStream_t)stream, no_launch));
     return GSR_OK;
 }
 

@@ -274,12 +274,13 @@ __device__ inline void old_load(const float *p, size_t base, bool acc, float (&o
 __device__ inline void gput_old(float *p, size_t idx, float v, bool acc, float old) { p[idx] = acc ? old + v : v; }
 
 // ------------------------------------------------------------------------------------------
-__device__ inline float3 dnormvdv(float3 v, float3 dv) {
-    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-    return make_float3(((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32,
-                       (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32,
-                       (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32);
+// Chain rule through u = v / |v|: du/dv = (|v|^2 I - v v^T) / |v|^3 applied to the gradient g.
+__device__ inline float3 unit_vec_bwd(float3 v, float3 g) {
+    const float n2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float inv_n3 = 1.0f / sqrtf(n2 * n2 * n2);
+    return make_float3(((+n2 - v.x * v.x) * g.x - v.y * v.x * g.y - v.z * v.x * g.z) * inv_n3,
+                       (-v.x * v.y * g.x + (n2 - v.y * v.y) * g.y - v.z * v.y * g.z) * inv_n3,
+                       (-v.x * v.z * g.x - v.y * v.z * g.y + (n2 - v.z * v.z) * g.z) * inv_n3);
 }
 
 // SH backward; writes all M coefficient rows of dL_dsh (zeros past the active degree).  `sh` and
@@ -359,7 +360,7 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos,
     const float3 dL_ddir = make_float3(dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2],
                                        dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
                                        dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]);
-    return dnormvdv(d0, dL_ddir);
+    return unit_vec_bwd(d0, dL_ddir);
 }
 
 __device__ inline void cov3d_backward(float3 s3, float mod, float4 q, const float *dc, float3 &dscale,
@@ -519,14 +520,14 @@ __device__ inline void gauss_bwd_one(
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) { qn = quat_norm(q); q = act_normalize(q, qn); }
         cov3d_from_scale_rot(s3, scale_modifier, q, c3);
     }
-    // ---- computeCov2DCUDA ----
+    // ---- dL/dconic -> dL/dSigma2D -> dL/dSigma3D, and the mean's share through J ----
     float3 t = xform4x3(mean, vm);
     const float limx = 1.3f * tan_fovx, limy = 1.3f * tan_fovy;
     const float txtz = t.x / t.z, tytz = t.y / t.z;
     t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
     t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
-    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
-    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+    const float keep_tx = txtz < -limx || txtz > limx ? 0 : 1;
+    const float keep_ty = tytz < -limy || tytz > limy ? 0 : 1;
     const m3 J = {{h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
                    -(h_y * t.y) / (t.z * t.z), 0, 0, 0}};
     const m3 Wm = {{vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]}};
@@ -536,13 +537,13 @@ __device__ inline void gauss_bwd_one(
     const float a = GM(c2, 0, 0) + 0.3f, b = GM(c2, 0, 1), c = GM(c2, 1, 1) + 0.3f;
     const float denom = a * c - b * b;
     float dL_da = 0, dL_db = 0, dL_dc = 0;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const float inv_det2 = 1.0f / ((denom * denom) + 0.0000001f);
     float dcov[6];
 #define TT(cc, rr) GM(T, cc, rr)
-    if (denom2inv != 0) {
-        dL_da = denom2inv * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
-        dL_dc = denom2inv * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
-        dL_db = denom2inv * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
+    if (inv_det2 != 0) {
+        dL_da = inv_det2 * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
+        dL_dc = inv_det2 * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
+        dL_db = inv_det2 * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
         dcov[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
         dcov[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
         dcov[5] = (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc);
@@ -582,14 +583,14 @@ __device__ inline void gauss_bwd_one(
     const float dJ12 = WW(2, 0) * dT10 + WW(2, 1) * dT11 + WW(2, 2) * dT12;
 #undef WW
     const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-    const float dL_dtx = x_grad_mul * -h_x * tz2 * dJ02;
-    const float dL_dty = y_grad_mul * -h_y * tz2 * dJ12;
+    const float dL_dtx = keep_tx * -h_x * tz2 * dJ02;
+    const float dL_dty = keep_ty * -h_y * tz2 * dJ12;
     const float dL_dtz = -h_x * tz2 * dJ00 - h_y * tz2 * dJ11 + (2 * h_x * t.x) * tz3 * dJ02 +
                          (2 * h_y * t.y) * tz3 * dJ12;
     float dm0 = vm[0] * dL_dtx + vm[1] * dL_dty + vm[2] * dL_dtz;
     float dm1 = vm[4] * dL_dtx + vm[5] * dL_dty + vm[6] * dL_dtz;
     float dm2 = vm[8] * dL_dtx + vm[9] * dL_dty + vm[10] * dL_dtz;
-    // ---- preprocessCUDA bwd: screen-space mean -> means3D ----
+    // ---- screen-space mean -> means3D through the projection ----
     const float4 mh = xform4x4(mean, pj);
     const float m_w = 1.0f / (mh.w + 0.0000001f);
     const float mul1 = (pj[0] * mean.x + pj[4] * mean.y + pj[8] * mean.z + pj[12]) * m_w * m_w;

@@ -82,7 +82,7 @@ def load_library():
     L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
                                vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]
     L.gsr_grad_fence.restype = i
-    L.gsr_grad_fence.argtypes = [vp, vp]
+    L.gsr_grad_fence.argtypes = [ctypes.POINTER(vp), i, vp]
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
     for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):
@@ -114,7 +114,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 9  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 10  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -311,13 +311,17 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     return out
 
 
-def grad_fence(means3D_grad):
-    """Declare that the work queued so far on the current stream writes the gradient set whose
-    means3D gradient is ``means3D_grad`` (an all-reduce, a reset): the next rasterizer backward
-    into that set, on any stream, is ordered after it (gsr_grad_fence)."""
-    dev = means3D_grad.device
+def grad_fence(*grads):
+    """Declare that the work queued so far on the current stream writes the gradient tensors
+    ``grads`` (an all-reduce, a reset of the bucket they live in): the next rasterizer backward
+    into any of them, on any stream, is ordered after it (gsr_grad_fence)."""
+    grads = [g for g in grads if g is not None and g.numel()]
+    if not grads:
+        return
+    dev = grads[0].device
+    arr = (ctypes.c_void_p * len(grads))(*[g.data_ptr() for g in grads])
     with _device_guard(dev):
-        _check(load_library().gsr_grad_fence(means3D_grad.data_ptr(), _stream_ptr(dev)))
+        _check(load_library().gsr_grad_fence(arr, len(grads), _stream_ptr(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

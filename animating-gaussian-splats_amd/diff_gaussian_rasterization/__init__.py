@@ -16,6 +16,7 @@ from typing import NamedTuple
 
 import torch
 import torch.nn as nn
+from torch.autograd.graph import get_gradient_edge
 
 from . import _C
 
@@ -38,17 +39,32 @@ class GaussianRasterizationSettings(NamedTuple):
     debug: bool = False
 
 
+def _engine_accumulates(t):
+    """True when the running backward pass will execute ``t``'s AccumulateGrad node, i.e. write
+    ``t.grad``: ``loss.backward()`` does; ``torch.autograd.grad(...)`` never does (the engine refuses
+    the query for its inputs) and ``loss.backward(inputs=[...])`` only for the listed leaves."""
+    try:
+        return bool(torch._C._will_engine_execute_node(get_gradient_edge(t).node))
+    except RuntimeError:  # autograd.grad(): the gradient is returned, .grad is left alone
+        return False
+
+
 def _accumulation_target(t):
     """The leaf's existing ``.grad`` when the backward kernel may add into it in place (and the
     Function then returns None for it): a leaf requiring grad whose gradient is a contiguous fp32
-    tensor of its shape, with no hooks that autograd's accumulation would have run.  Gives the same
-    value as autograd's AccumulateGrad (one fp32 add) without its separate read-read-write pass."""
+    tensor of its shape, with no hooks that autograd's accumulation would have run, in a backward
+    pass that will accumulate into that leaf (``_engine_accumulates``) without building a graph of
+    the gradient (``create_graph``).  Gives the same value as autograd's AccumulateGrad (one fp32
+    add, ``grad += new``) without its separate read-read-write pass; every other case returns the
+    gradient to autograd as stock Functions do."""
     if t is None or not isinstance(t, torch.Tensor) or t.numel() == 0 or not t.is_leaf or not t.requires_grad:
         return None
     g = t.grad
     if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != t.shape or g.requires_grad:
         return None
     if t._backward_hooks or getattr(t, "_post_accumulate_grad_hooks", None):
+        return None
+    if torch.is_grad_enabled() or not _engine_accumulates(t):
         return None
     return g
 

@@ -8,7 +8,7 @@ Drop-ins with the reference's names, signatures and effects:
   -- external.py:211-314: every 100 iterations in [500, 5000] clone small high-gradient Gaussians,
   split large ones in two, drop the split originals, prune transparent (and from i = 3000 huge)
   ones, with the optimizer's Adam moments carried along (``cat_params_to_optimizer`` /
-  ``remove_points``, external.py:144-204) and the statistics reset; every 3000 iterations reset the
+  ``remove_points``, external.py:144-204) and the statistics reset; at i = 3000 reset the
   opacities (external.py:306-314).
 
 The reference runs ~60 torch ops per densification, reallocating every parameter and both Adam
@@ -199,24 +199,29 @@ def _densify(params, dv, scene_radius, optimizer, i, sample_fn):
 
 
 def densify_gaussians(gaussian_cloud_parameters, densification_variables, scene_radius, optimizer, i,
-                      sample_fn=None):
+                      sample_fn=None, accumulate=True):
     """external.py:211-314.  ``sample_fn`` (optional, default ``torch.normal``) draws the split
-    samples; tests pass the reference's recorded draw.  Returns the row counts when this call
-    densified, else None."""
+    samples; tests pass the reference's recorded draw, the data-parallel path a rank-0 draw broadcast
+    to every rank (splat_dp.broadcast_normal).  ``accumulate=False`` skips the per-call
+    accumulate_mean_2d_gradients (external.py:219) for callers that accumulated their views' statistics
+    already (splat_dp.DensifyStats).  Returns the row counts when this call densified, else None."""
     info = None
     if i <= 5000:
-        accumulate_mean_2d_gradients(densification_variables)
+        if accumulate:
+            accumulate_mean_2d_gradients(densification_variables)
         if (i >= 500) and (i % 100 == 0):
             info = _densify(gaussian_cloud_parameters, densification_variables, scene_radius, optimizer, i,
                             sample_fn)
-    if i > 0 and i % 3000 == 0:  # opacity reset (external.py:306-314): a new tensor, zeroed moments
-        p = gaussian_cloud_parameters["opacity_logits"]
-        new = inverse_sigmoid(torch.ones_like(p) * 0.01)
-        group = _group_of(optimizer, "opacity_logits")
-        stored = optimizer.state.get(group["params"][0], None)
-        if stored is not None:
-            _install(gaussian_cloud_parameters, optimizer, "opacity_logits", new, torch.zeros_like(new),
-                     torch.zeros_like(new))
-        else:
-            _install(gaussian_cloud_parameters, optimizer, "opacity_logits", new, None, None)
+        if i > 0 and i % 3000 == 0:
+            # opacity reset (external.py:306-314, nested in `if i <= 5000`: it fires at i = 3000 only):
+            # a new tensor, zeroed moments
+            p = gaussian_cloud_parameters["opacity_logits"]
+            new = inverse_sigmoid(torch.ones_like(p) * 0.01)
+            group = _group_of(optimizer, "opacity_logits")
+            stored = optimizer.state.get(group["params"][0], None)
+            if stored is not None:
+                _install(gaussian_cloud_parameters, optimizer, "opacity_logits", new, torch.zeros_like(new),
+                         torch.zeros_like(new))
+            else:
+                _install(gaussian_cloud_parameters, optimizer, "opacity_logits", new, None, None)
     return info

@@ -16,6 +16,11 @@ reproduces the single-process result exactly (up to summation order):
                        reference's own formulas, then SUM (norm accumulator, visibility count) / MAX
                        (radii) reductions before the clone/split/prune decision, so every rank takes
                        identical densification decisions
+* ``broadcast_normal`` the split samples (external.py:260-261 ``torch.normal``) drawn on one rank and
+                       broadcast, so the split copies -- and from then on every parameter -- stay
+                       identical on all ranks
+* ``densify_gaussians`` the DP densification step: all-reduced statistics + broadcast samples around
+                       ``splat_densify.densify_gaussians``
 
 The data path has exactly one collective per step (the gradient all-reduce); the densify-stat
 reduction runs only when densification happens (every 100 iterations in densify.py).
@@ -148,3 +153,37 @@ class DensifyStats:
         self.visibility_count.copy_(packed[1])
         dist.all_reduce(self.max_2d_radii, op=dist.ReduceOp.MAX, group=group)
         return self
+
+
+def broadcast_normal(group=None, src: int = 0):
+    """A ``sample_fn`` for ``splat_densify.densify_gaussians``: ``torch.normal(mean, std)`` drawn on
+    rank ``src`` only and broadcast to every rank.  The reference draws the split offsets with an
+    unseeded ``torch.normal`` (external.py:260-261); drawn independently per rank they would make the
+    replicas' split copies -- and every later gradient -- diverge."""
+    def draw(mean, std):
+        if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+            return torch.normal(mean=mean, std=std)
+        out = torch.normal(mean=mean, std=std) if dist.get_rank(group) == src else torch.empty_like(std)
+        dist.broadcast(out, src=src, group=group)
+        return out
+    return draw
+
+
+def densify_gaussians(params, stats: "DensifyStats", scene_radius, optimizer, i, group=None, densify_fn=None):
+    """Camera-DP densification (densify.py:218-247 + external.py:211-314 on sharded views): the
+    ranks' view statistics are reduced (``DensifyStats.allreduce``: SUM, SUM, MAX) and handed to
+    ``densify_fn`` (default ``splat_densify.densify_gaussians`` with ``accumulate=False`` -- the views
+    were accumulated by ``stats.update``) together with a ``broadcast_normal`` sampler, so every rank
+    makes the same clone / split / prune decisions and draws the same split offsets."""
+    stats.allreduce(group)
+    if densify_fn is None:
+        import splat_densify
+        dv = splat_densify.DensificationVariables(visibility_count=stats.visibility_count,
+                                                  mean_2d_gradients_accumulated=stats.mean_2d_gradients_accumulated,
+                                                  max_2d_radii=stats.max_2d_radii)
+        info = splat_densify.densify_gaussians(params, dv, scene_radius, optimizer, i,
+                                               sample_fn=broadcast_normal(group), accumulate=False)
+        stats.visibility_count, stats.mean_2d_gradients_accumulated, stats.max_2d_radii = \
+            dv.visibility_count, dv.mean_2d_gradients_accumulated, dv.max_2d_radii
+        return info
+    return densify_fn(params, stats, scene_radius, optimizer, i, broadcast_normal(group))

@@ -1,6 +1,6 @@
 """One densify.py iteration on the native path (the caller side of SURVEY.md 8(a) + rows 8(f) 1-3).
 
-``densify_iteration`` is the body of densify.py's loop (densify.py:234-258) with every piece on the
+``densify_iteration`` is the body of densify.py's loop (densify.py:218-247) with every piece on the
 HIP kernels of ``libgsr.so``:
 
 =====================================================  ============================================
@@ -50,7 +50,7 @@ def create_densification_variables(params):
 
 
 def densify_iteration(params, view, densification_variables, optimizer, scene_radius, i, sample_fn=None):
-    """densify.py:234-258 for one view.  Returns (total_loss, image_loss, segmentation_loss) as
+    """densify.py:218-247 for one view.  Returns (total_loss, image_loss, segmentation_loss) as
     detached scalars (no host sync) and the densify row counts when this iteration densified."""
     rs = view.render_settings
     dv = densification_variables

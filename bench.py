@@ -66,28 +66,35 @@ def calibrated_traffic(pm, phase, P, K, N, T):
 
 
 def algorithmic_bytes(phase, P, K, N, T, F, sh):
-    """Compulsory HBM bytes of one launch of each kernel (DESIGN.md 'Kernels and their rooflines')."""
-    if phase == "preprocess":      # read means/scales/rot/opacity/features, write 7 SoA records
-        return P * (44 + F) + P * 60
+    """Compulsory HBM bytes of one launch of each kernel: its share of SURVEY.md 8(d)'s per-view byte
+    model (one sort pass, no atomics, no scratch records -- the backward's per-pair partial records
+    replace the reference's atomics and are this design's own traffic, not algorithmic)."""
+    if phase == "preprocess":      # read means/scales/rot/opacity/features, write the geometry records
+        return P * (44 + F) + P * (36 + 12 * sh)
     if phase == "render_fwd":      # per pair: id + xy + conic/op + rgb/depth gather; per pixel outputs
-        return K * 44 + N * 24 + T * 12
-    if phase == "render_bwd":      # per pair: id + emission slot + 36 B gather + 36 B partial record
-        return K * (4 + 4 + 36 + 36) + N * 20 + T * 12
-    if phase == "gauss_bwd":       # per Gaussian inputs + all gradient outputs; per pair 36 B record
-        return P * (44 + F + 12) + P * (56 + F) + K * 36
-    if phase == "tile_sort":       # (depth|id) key + emission index in, point list + slot map out
-        return K * (8 + 4 + 4 + 4)
-    if phase == "bin_emit":        # rect + tile count + depth + offset per Gaussian; key + index out
-        return P * (16 + 4 + 4) + K * 12
-    if phase == "bin_count":
-        return P * 12 + T * 4
+        return K * 44 + N * 24 + T * 16
+    if phase == "render_bwd":      # per pair: 40 B gather; per pixel: dL/dpix + final T + n_contrib
+        return K * 40 + N * 20 + T * 16
+    if phase == "gauss_bwd":       # per Gaussian: inputs read + every gradient written
+        return P * (84 + F) + P * (56 + F)
+    if phase == "tile_sort":       # one sort pass over the pairs
+        return K * 24
+    if phase == "bin_emit":        # duplicate with keys: 12 B per emitted pair
+        return K * 12
     return 0
 
 
+def pipeline_bytes(P, K, N, T, F, sh):
+    """B = P (220 + 3F + 12 [SH]) + 120 K + 44 N + 16 T per fwd + bwd of one view."""
+    return P * (220 + 3 * F + 12 * sh) + 120 * K + 44 * N + 16 * T
+
+
 def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu):
-    """Single-threaded C oracle, forward + backward of ONE view of the same workload."""
+    """The C oracle (OpenMP over tiles / Gaussians, OMP_NUM_THREADS threads), forward + backward of ONE
+    view of the same workload on this host's cores."""
     from oracle import oracle as O
     import splat_scenes as S
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     a = {k: (v.detach().numpy() if isinstance(v, torch.Tensor) else v)
          for k, v in S.activated_inputs(params_cpu, cfg.sh_degree).items()}
     t0 = time.perf_counter()
@@ -97,10 +104,12 @@ def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu):
                    a.get("shs"), cam_cpu.sh_degree, cam_cpu.campos.numpy())
     O.backward(st, dl_cpu.numpy())
     dt = time.perf_counter() - t0
-    return {"value": round(cfg.P / dt / 1e6, 6), "unit": "Msplats/s", "cores": 1, "kind": "port",
+    return {"value": round(cfg.P / dt / 1e6, 6), "unit": "Msplats/s", "cores": threads, "kind": "port",
+            "host_nproc": os.cpu_count(),
             "sample": f"1 view of the same workload ({cfg.P} Gaussians, {cam_cpu.image_width}x"
-                      f"{cam_cpu.image_height}, SH{cfg.sh_degree}) fwd+bwd by the single-threaded C "
-                      f"oracle (oracle/gsr_oracle.c), {dt:.1f} s"}
+                      f"{cam_cpu.image_height}, SH{cfg.sh_degree}) fwd+bwd by the C oracle "
+                      f"(oracle/gsr_oracle.c, OpenMP, {threads} threads of {os.cpu_count()} host CPUs), "
+                      f"{dt:.2f} s"}
 
 
 def _torch_calc_ssim(img1, img2):
@@ -209,7 +218,7 @@ def _torch_densify_event(params, acc, cnt, scene_radius, opt, i):
 
 
 def densify_call_site(steps, cfg, cam, dev):
-    """densify.py's loop body (densify.py:234-258) at the bench resolution on a 1M-Gaussian
+    """densify.py's loop body (densify.py:218-247) at the bench resolution on a 1M-Gaussian
     densify.py-style parameter dict: (a) the native path (splat_train.densify_iteration: fused
     activations, fused L1+SSIM, statistics kernels, FusedAdam) vs (b) the reference's composition
     (torch activations + this rasterizer + torch calc_ssim / l1 + torch statistics + torch.optim.Adam),
@@ -276,12 +285,21 @@ def densify_call_site(steps, cfg, cam, dev):
     nat = timed(native, nat_state, 501)
     ref_state = fresh(torch.optim.Adam)
     ref = timed(reference, ref_state, 501)
-    # one densification event each way, on the statistics the timed iterations accumulated
+    # One densification event each way on the statistics the timed iterations accumulated, scaled so
+    # that 20 % of the seen Gaussians pass the 0.0002 gradient threshold, with a scene radius that puts
+    # the 0.01 r clone / split boundary at the cloud's median maximum scale: clones AND splits happen
+    # (with the bench's tiny synthetic gradients and r = 4 nothing would split).
     out = {"gaussians": P, "image": f"{W}x{H}", "native_iteration_ms": round(nat, 3),
            "reference_composition_iteration_ms": round(ref, 3), "steps": steps}
+    dv0 = nat_state[2]
+    seen = dv0.visibility_count > 0
+    avg = dv0.mean_2d_gradients_accumulated[seen] / dv0.visibility_count[seen]
+    gscale = float(2e-4 / torch.quantile(avg[:1 << 24].float(), 0.8).clamp_min(1e-30))
+    radius = float(100.0 * torch.exp(nat_state[0]["log_scales"].detach()).max(dim=1).values.median())
+    out["densify_event"] = {"gradient_scale": gscale, "scene_radius": radius}
     for name, state in (("native", nat_state), ("reference", ref_state)):
         params, opt, dv = state
-        acc, cnt = dv.mean_2d_gradients_accumulated.clone(), dv.visibility_count.clone()
+        acc, cnt = dv.mean_2d_gradients_accumulated * gscale, dv.visibility_count.clone()
         torch.cuda.synchronize()
         t = time.perf_counter()
         if name == "native":
@@ -289,9 +307,9 @@ def densify_call_site(steps, cfg, cam, dev):
             _C.profile_select(["densify_plan", "densify_apply"])
             _C.profile_enable(True)
             dv.mean_2d_gradients_accumulated, dv.visibility_count = acc, cnt
-            info = splat_densify._densify(params, dv, 4.0, opt, 600, None)
+            info = splat_densify._densify(params, dv, radius, opt, 600, None)
         else:
-            _torch_densify_event(params, acc, cnt, 4.0, opt, 600)
+            _torch_densify_event(params, acc, cnt, radius, opt, 600)
         torch.cuda.synchronize()
         out[f"{name}_densify_event_ms"] = round((time.perf_counter() - t) * 1e3, 3)
         if name == "native":
@@ -386,15 +404,68 @@ def io_call_site(timesteps, dev, W=640, H=360, C=27):
         shutil.rmtree(root, ignore_errors=True)
 
 
+def _self_launch(n):
+    """``--gpus N`` without a launcher: start N ranks with torch.distributed.run (127.0.0.1 rendezvous)
+    as CHILD processes and relay their output (rank 0 prints the JSON line).  The parent never touches
+    the GPU and never re-execs; it exits with the launcher's status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def _dry_run(args, rank, world):
+    """CPU rehearsal of the launcher and the step's control flow (no GPU, gloo): shard the config's
+    views, fill a gradient bucket per view, all-reduce it once per step, report what every rank did."""
+    import torch.distributed as dist
+    import splat_dp
+    import splat_scenes as S
+    views = list(range(len(S.RIG27)))
+    mine = splat_dp.shard_views(views, rank, world) if args.config == "C4" else \
+        splat_dp.shard_views([(k) % len(views) for k in range(world * args.views_per_rank)], rank, world)
+    bucket = torch.zeros(16)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bucket.zero_()
+        for v in mine:
+            bucket += float(v + 1)
+        if world > 1:
+            dist.all_reduce(bucket)
+    elapsed = time.perf_counter() - t0
+    shards = [None] * world
+    if world > 1:
+        dist.all_gather_object(shards, mine)
+    else:
+        shards = [mine]
+    expect = float(sum(v + 1 for sh in shards for v in sh))
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (launcher + sharding + collective rehearsal, no GPU)", "value": None,
+                          "unit": None, "n_gpus": world, "steps": args.steps, "dry_run": True,
+                          "config": {"workload": args.config, "views_per_rank": [len(x) for x in shards]},
+                          "bucket_sum_ok": bool(torch.all(bucket == expect)),
+                          "ms_per_step": round(elapsed / max(args.steps, 1) * 1e3, 4)}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C3", choices=["C3", "C4", "C5"],
+                    help="C3 (default): 1M Gaussians SH3 at 1080p, --views-per-rank rig views per GPU per "
+                         "step (weak scaling); C4: 1M Gaussians, the 27-camera rig sharded round-robin over "
+                         "the ranks per step + one RCCL SUM all-reduce (strong scaling); C5: 2M Gaussians x "
+                         "150-frame sequence, frames sharded in blocks, one per-frame optimisation iteration "
+                         "(5 views, fused L1+SSIM, fused Adam) per GPU per step, no collective (weak scaling)")
     ap.add_argument("--views-per-rank", type=int, default=5,
-                    help="views rendered per GPU per step (train.py:757 sums the losses of 5 views "
-                         "per optimisation step)")
-    ap.add_argument("--config", default="C3")
+                    help="C3 / C5: views rendered per GPU per step (train.py:753 optimises on the summed "
+                         "losses of 5 views per step)")
     ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the step's views alternate over: one view's memory-bound "
                          "per-Gaussian backward overlaps the next view's VALU-bound render kernels; "
@@ -402,26 +473,39 @@ def main():
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path on one GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launcher / sharding / collective (gloo, no GPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--call-site-steps", type=int, default=10,
-                    help="steps timed for each train.py call-site variant (0 = skip)")
+                    help="steps timed for each train.py call-site variant (0 = skip; N = 1, C3 only)")
     ap.add_argument("--loss-steps", type=int, default=10,
-                    help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip)")
+                    help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip; N = 1, C3)")
     ap.add_argument("--densify-steps", type=int, default=5,
-                    help="densify.py iterations timed per variant at the bench resolution (0 = skip)")
+                    help="densify.py iterations timed per variant at the bench resolution (0 = skip; N = 1, C3)")
     ap.add_argument("--io-timesteps", type=int, default=2,
                     help="timesteps of 27 synthetic 640x360 frames loaded per variant by the data-path "
-                         "leg (0 = skip)")
+                         "leg (0 = skip; N = 1, C3)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="untimed steps with events on every phase (per-kernel breakdown)")
     args = ap.parse_args()
 
-    import splat_scenes as S
-    from diff_gaussian_rasterization import GaussianRasterizer, _C
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args.gpus))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        _dry_run(args, rank, world)
+        return
+
+    import splat_dp
+    import splat_scenes as S
+    from diff_gaussian_rasterization import GaussianRasterizer, _C, rasterize_parameters
+
     dist = None
     local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several gloo ranks on one GPU
     if world > 1:
@@ -431,45 +515,56 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(args.backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     _C.load_library()
 
-    base = S.CONFIGS[args.config]
-    cfg = S.SceneConfig(base.name, base.P, base.width, base.height, base.focal, base.s0,
-                        sh_degree=base.sh_degree, views=S.RIG27)
+    if args.config == "C5":
+        cfg = S.SceneConfig("C5", 2_000_000, 1920, 1080, 1600.0, 0.005, views=S.RIG27)
+    else:
+        base = S.CONFIGS[args.config]
+        cfg = S.SceneConfig(base.name, base.P, base.width, base.height, base.focal, base.s0,
+                            sh_degree=base.sh_degree, views=S.RIG27)
     params_cpu = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0, device="cpu")
     params = {k: torch.nn.Parameter(v.to(dev)) for k, v in params_cpu.items()}
     cams = S.scene_cameras(cfg, device=dev)
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
     V = args.views_per_rank
 
-    import splat_dp
-    from diff_gaussian_rasterization import rasterize_parameters
     # the rasterizer's inputs: render arguments of shared.py:29-42, activated once, as leaves
     with torch.no_grad():
         act = S.activated_inputs(params, cfg.sh_degree)
     if cfg.sh_degree >= 0:
         act.pop("colors_precomp")
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
-    # N > 1: the gradients live in one flat bucket that backward accumulates into and RCCL reduces
-    # in place (no pack / unpack copies)
+    grads_of = lambda: [v.grad for k, v in leaves.items() if k != "means2D"]  # noqa: E731
+    # N > 1 (C3 / C4): the gradients live in one flat bucket that backward accumulates into and RCCL
+    # reduces in place (no pack / unpack copies)
     reducer = splat_dp.GradAllReduce([v for k, v in leaves.items() if k != "means2D"]).attach() \
-        if dist is not None else None
+        if dist is not None and args.config != "C5" else None
 
-    def views_of(it):
-        # rank r renders its round-robin share of this step's world * V rig cameras
-        return splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)],
-                                    rank, world)
+    if args.config == "C4":  # the whole rig every step, sharded round-robin (4,4,4,3,3,3,3,3 at 8)
+        views_per_step = len(cams)
+        my_views = splat_dp.shard_views(list(range(len(cams))), rank, world)
 
-    main = torch.cuda.current_stream(dev)
+        def views_of(it):
+            return my_views
+    else:
+        views_per_step = world * V
+
+        def views_of(it):  # rank r renders its round-robin share of this step's world * V rig cameras
+            return splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)], rank, world)
+
+    main_stream = torch.cuda.current_stream(dev)
     # side streams for the views: the main stream keeps the collectives (N > 1) out of their way
     streams = [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1))]
     for s in streams:
-        s.wait_stream(main)  # the setup's parameters, leaves and upstream gradient
+        s.wait_stream(main_stream)  # the setup's parameters, leaves and upstream gradient
 
     if reducer is not None:  # the bucket's zeroing (main stream) precedes the first backward
-        _C.grad_fence(leaves["means3D"].grad)
+        _C.grad_fence(*grads_of())
 
     def step(it):
         # No stream waits for another at the step start: libgsr orders the gradient writes across
@@ -482,14 +577,20 @@ def main():
                 img.backward(dl)
         if reducer is not None:
             for s in streams:
-                main.wait_stream(s)
+                main_stream.wait_stream(s)
             reducer.reduce()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
             reducer.zero_()
-            _C.grad_fence(leaves["means3D"].grad)
+            _C.grad_fence(*grads_of())
             leaves["means2D"].grad = None
         else:
             for p in leaves.values():
                 p.grad = None
+
+    c5 = None
+    if args.config == "C5":
+        c5 = _C5Fit(cfg, params_cpu, cams, rank, world, V, dev, streams, main_stream,
+                    args.warmup + args.probe_steps + args.steps)
+        step = c5.step  # noqa: F811
 
     def step_reference_call_site(it):  # train.py: create_render_arguments + Renderer + backward
         for ci in views_of(it):
@@ -553,8 +654,9 @@ def main():
     # dominant kernel's device time inside the timed region (HIP events on its launch stream)
     tot_ms, cnt = _C.profile_read(dom)
     _C.profile_select(None)
+    legs = world == 1 and args.config == "C3"
     call_site = None
-    if args.call_site_steps > 0:
+    if legs and args.call_site_steps > 0:
         first = args.warmup + args.probe_steps
         per_view = len(views_of(first))
         time_steps(step_reference_call_site, 3, first)  # warm each path's kernels and allocations
@@ -565,17 +667,16 @@ def main():
                      "fused_activations_ms_per_view": round(fused_ms / per_view, 4),
                      "steps": args.call_site_steps}
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
-    loss_site = loss_call_site(args.loss_steps, cams[0], leaves, dev) if args.loss_steps > 0 else None
-    dens_site = densify_call_site(args.densify_steps, cfg, cams[0], dev) if args.densify_steps > 0 else None
-    io_site = io_call_site(args.io_timesteps, dev) if args.io_timesteps > 0 and rank == 0 else None
+    loss_site = loss_call_site(args.loss_steps, cams[0], leaves, dev) if legs and args.loss_steps > 0 else None
+    dens_site = densify_call_site(args.densify_steps, cfg, cams[0], dev) if legs and args.densify_steps > 0 else None
+    io_site = io_call_site(args.io_timesteps, dev) if legs and args.io_timesteps > 0 else None
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
-    import splat_dp
-    used = sorted({ci for it in range(args.warmup + args.probe_steps, args.warmup + args.probe_steps + args.steps)
-                   for ci in splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)],
-                                                  rank, world)})
+    first = args.warmup + args.probe_steps
+    used = c5.used_views(first, args.steps) if c5 else \
+        sorted({ci for it in range(first, first + args.steps) for ci in views_of(it)})
     Ks = []
     with torch.no_grad():
-        a = S.activated_inputs(params, cfg.sh_degree)
+        a = c5.frame_inputs(c5.frames[0]) if c5 else S.activated_inputs(params, cfg.sh_degree)
         if cfg.sh_degree >= 0:
             a.pop("colors_precomp")
         e = torch.empty(0, device=dev)
@@ -591,16 +692,16 @@ def main():
     N = cfg.width * cfg.height
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
     F = 12 * (cfg.sh_degree + 1) ** 2 if cfg.sh_degree >= 0 else 12
+    SH = int(cfg.sh_degree >= 0)
     avg_ms = tot_ms / max(cnt, 1)
     traffic = traffic_2x = None
     if os.path.exists(PMC_SUMMARY):
         pm = json.load(open(PMC_SUMMARY)).get("k_" + dom)
-        if pm:
+        if pm and args.config == "C3":
             traffic_2x = int(pm["hbm_bytes_per_launch_corrected"])
-            traffic = calibrated_traffic(pm, dom, cfg.P, K, cfg.width * cfg.height,
-                                         ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16))
+            traffic = calibrated_traffic(pm, dom, cfg.P, K, N, T)
     valu = None
-    if os.path.exists(SQ_SUMMARY):
+    if os.path.exists(SQ_SUMMARY) and args.config == "C3":
         q = json.load(open(SQ_SUMMARY)).get("k_" + dom)
         if q and "SQ_INSTS_VALU" in q:
             # the kernel's wave64 VALU instructions (profile of this command) over its live duration,
@@ -613,11 +714,12 @@ def main():
                     "achieved_Ginst_s": round(rate, 1), "peak_Ginst_s": VALU_PEAK_GINST,
                     "issue_frac": round(rate / VALU_PEAK_GINST, 4),
                     "source": os.path.relpath(SQ_SUMMARY, REPO)}
-    bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, cfg.sh_degree >= 0)
+    bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, SH)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * V * cfg.P / (elapsed / args.steps) / 1e6
+    value = views_per_step * cfg.P / (elapsed / args.steps) / 1e6
+    pipe_b = pipeline_bytes(cfg.P, K, N, T, F, SH)
+    pipe_gbps = pipe_b * views_per_step / world / (elapsed / args.steps) / 1e9
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -626,25 +728,46 @@ def main():
                                         S.look_at(yaw, hgt, cfg.distance), device="cpu",
                                         sh_degree=max(cfg.sh_degree, 0))
             cpu = cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl.cpu())
+        workload = {
+            "C3": f"C3: {cfg.P} Gaussians, SH{cfg.sh_degree}, {cfg.width}x{cfg.height}, 27-camera rig, "
+                  f"{V} view(s)/GPU/step, fwd+bwd" + (", RCCL SUM all-reduce of the gradients" if world > 1 else ""),
+            "C4": f"C4: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, the 27-camera rig per step sharded "
+                  f"round-robin over {world} GPU(s), fwd+bwd" + (", one RCCL SUM all-reduce" if world > 1 else ""),
+            "C5": f"C5: {cfg.P} Gaussians x 150 frames, RGB, {cfg.width}x{cfg.height}, frames sharded in blocks "
+                  f"over {world} GPU(s); one per-frame optimisation iteration per GPU per step = {V} rig views "
+                  f"fwd + fused L1/SSIM + bwd + fused Adam; no collective",
+        }[args.config]
         out = {
-            "metric": "Msplats/sec fwd+bwd @1080p (1M gauss)",
+            "metric": "Msplats/sec fwd+bwd @1080p (1M gauss)" if args.config != "C5" else
+                      "Msplats/sec fwd+bwd @1080p (2M gauss per-frame fits)",
             "value": round(value, 3), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"{cfg.name}: {cfg.P} Gaussians, SH{cfg.sh_degree}, "
-                                   f"{cfg.width}x{cfg.height}, 27-camera rig, {V} view(s)/GPU/step, fwd+bwd",
-                       "gaussians": cfg.P, "views_per_gpu_per_step": V,
+            "scaling": "strong" if args.config == "C4" else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": workload, "gaussians": cfg.P, "views_per_step": views_per_step,
+                       "views_per_gpu": [len(splat_dp.shard_views(list(range(views_per_step)), r, world))
+                                         for r in range(world)],
                        "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
-                       "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}",
-                       "streams_per_gpu": len(streams)},
+                       "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}" if args.config != "C5"
+                       else f"frame-dp{world}", "streams_per_gpu": len(streams),
+                       "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
                          "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if traffic else None,
                          "traffic_2x_fetch": traffic_2x,
-                         "traffic_calibration": "profiles/r01_fetch_calib.txt",
+                         "traffic_calibration": "profiles/r01_fetch_calib.txt" if traffic else None,
                          "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch),
-                         "valu": valu},
+                         "algorithmic_bytes_formula": {"render_bwd": "K*40 + N*20 + T*16",
+                                                       "render_fwd": "K*44 + N*24 + T*16",
+                                                       "gauss_bwd": "P*(84+F) + P*(56+F)"}.get(dom),
+                         "binding_resource": "VALU issue (blend evaluations: ~256 pixel-Gaussian pairs per "
+                                             "pair record); HBM traffic is a small share of the kernel time",
+                         "valu": valu,
+                         "pipeline": {"bytes_per_view": int(pipe_b),
+                                      "formula": "P*(220 + 3F + 12*SH) + 120*K + 44*N + 16*T (SURVEY.md 8(d))",
+                                      "achieved_GBps_per_gpu": round(pipe_gbps, 1),
+                                      "frac": round(pipe_gbps / HBM_PEAK_GBPS, 4)}},
             "phase_ms_per_launch": {ph: round(probe[ph][0] / max(probe[ph][1], 1), 5) for ph in PHASES},
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
@@ -656,6 +779,76 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+class _C5Fit:
+    """BASELINE.json configs[4]: per-frame optimisation of a 2M-Gaussian cloud over a 150-frame
+    dynamic sequence (frame t displaces the means by 0.05 sin(2 pi t / 150 + phi_i),
+    phi ~ U(0, 2 pi) seed 2), frames sharded over the ranks in contiguous blocks (splat_dp.shard_frames;
+    independent fits, no exchange).  One step = one optimisation iteration of this rank's current frame
+    as train.py runs it (train.py:738-776: render 5 views, L1 + SSIM losses, backward, Adam step):
+    5 rig views through rasterize_parameters (fused activations), the fused L1 + SSIM loss against the
+    frame's target images (renders of the frame's ground-truth cloud, made before timing: the
+    captured images of a real sequence are resident too), backward per view on the HIP streams, one
+    FusedAdam step (densify.py:68-86 learning rates)."""
+
+    def __init__(self, cfg, params_cpu, cams, rank, world, V, dev, streams, main_stream, total_steps):
+        import math
+        import splat_adam
+        import splat_dp
+        from diff_gaussian_rasterization import rasterize_parameters
+        self.cams, self.V, self.dev, self.streams, self.main = cams, V, dev, streams, main_stream
+        self.rasterize = rasterize_parameters
+        g = torch.Generator().manual_seed(2)
+        self.phi = (torch.rand(cfg.P, 1, generator=g) * 2 * math.pi).to(dev)
+        self.base = {k: v.to(dev) for k, v in params_cpu.items()}
+        self.frames = list(splat_dp.shard_frames(150, rank, world))
+        self.params = {k: torch.nn.Parameter(v.clone()) for k, v in self.base.items()}
+        lrs = {"means": 0.00016, "colors": 0.0025, "rotation_quaternions": 0.001, "opacity_logits": 0.05,
+               "log_scales": 0.001}
+        self.opt = splat_adam.FusedAdam([{"params": [p], "name": k, "lr": lrs.get(k, 1e-3)}
+                                         for k, p in self.params.items()], lr=0.0, eps=1e-15)
+        self.targets = {}
+        with torch.no_grad():
+            for it in range(min(total_steps, len(self.frames))):
+                f = self.frames[it]
+                gt = self.frame_params(f)
+                for ci in self.frame_views(f):
+                    self.targets[(f, ci)] = rasterize_parameters(gt, cams[ci])[0].detach()
+        torch.cuda.synchronize()
+
+    def frame_params(self, t):
+        import math
+        p = dict(self.base)
+        p["means"] = self.base["means"] + 0.05 * torch.sin(2 * math.pi * t / 150 + self.phi)
+        return p
+
+    def frame_inputs(self, t):
+        import splat_scenes as S
+        return S.activated_inputs(self.frame_params(t), -1)
+
+    def frame_views(self, t):
+        return [(t * self.V + j) % len(self.cams) for j in range(self.V)]
+
+    def used_views(self, first, n):
+        return sorted({ci for it in range(first, first + n) for ci in self.frame_views(self.frames[it % len(self.frames)])})
+
+    def step(self, it):
+        import splat_loss
+        f = self.frames[it % len(self.frames)]
+        for s in self.streams:
+            s.wait_stream(self.main)  # the previous iteration's Adam update
+        for k, ci in enumerate(self.frame_views(f)):
+            with torch.cuda.stream(self.streams[k % len(self.streams)]):
+                img = self.rasterize(self.params, self.cams[ci])[0]
+                tgt = self.targets.get((f, ci))
+                if tgt is None:
+                    raise RuntimeError(f"C5: no target for frame {f} view {ci}")
+                splat_loss.image_loss(img, tgt).backward()
+        for s in self.streams:
+            self.main.wait_stream(s)
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
 
 
 if __name__ == "__main__":

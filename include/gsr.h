@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 9
+#define GSR_ABI_VERSION 10
 
 enum gsr_status {
     GSR_OK = 0,
@@ -145,12 +145,14 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
                  const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
                  void *stream);
 
-/* Cross-stream order of gradient writes (ABI >= 9).  gsr_backward calls that write the same
- * gradient outputs (identified by out->dL_dmeans3D) on different streams are ordered behind each
- * other by the library.  gsr_grad_fence declares that the work queued so far on `stream` also
- * writes those outputs (e.g. an all-reduce or a reset of the gradient bucket), so the next
- * gsr_backward into them, on any stream, waits for it -- and the streams themselves need not. */
-int gsr_grad_fence(const float *dL_dmeans3D, void *stream);
+/* Cross-stream order of gradient writes (ABI >= 10).  gsr_backward calls that write the same
+ * gradient array (any of the gsr_grads pointers, accumulated or not) from different streams are
+ * ordered behind each other by the library: each write waits for the previous writer of every
+ * array it touches when that writer ran on another stream.  gsr_grad_fence declares that the work
+ * queued so far on `stream` also writes the `n` arrays `grads` (e.g. an all-reduce or a reset of the
+ * gradient bucket they live in), so the next gsr_backward into any of them, on any stream, waits
+ * for it -- and the streams themselves need not. */
+int gsr_grad_fence(const void *const *grads, int n, void *stream);
 
 /* present[i] = Gaussian i passes the near-plane frustum test (view-space z > 0.2). */
 int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const float *projmatrix,

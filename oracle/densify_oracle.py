@@ -11,7 +11,7 @@ Restates, array by array:
     high-gradient Gaussians, split large ones into two samples of N(0, scale) rotated by
     ``build_rotation`` (:27-46) with scales / 1.6, drop the split originals, prune by opacity (and
     big world-space scale from i = 3000), reset Adam moments of new rows to zero, reset the
-    statistics, and reset opacities every 3000 iterations.
+    statistics, and reset opacities at i = 3000 (the reset sits inside ``if i <= 5000``).
 
 The split samples are an input (the reference draws them with ``torch.normal``; the tests feed the
 values the reference drew).  Pinned against the reference's own outputs in
@@ -98,6 +98,8 @@ def densify(params, m, v, acc, count, max_radii, vis, m2grad, scene_radius, i, s
             to_split = (padded >= thr) & (np.exp(params["log_scales"]).max(axis=1) > small)
             S = int(to_split.sum())
             stds = np.tile(np.exp(params["log_scales"])[to_split], (2, 1))
+            if callable(samples):  # drawn now from the split rows' stds (e.g. a broadcast draw)
+                samples = np.asarray(samples(stds), np.float32)
             assert samples.shape == (2 * S, 3), (samples.shape, S)
             new = {k: np.tile(params[k][to_split], (2, 1)) for k in keys}
             rots = np.tile(build_rotation(params["rotation_quaternions"][to_split]), (2, 1, 1))
@@ -130,10 +132,10 @@ def densify(params, m, v, acc, count, max_radii, vis, m2grad, scene_radius, i, s
                     m[k], v[k] = m[k][keep], v[k][keep]
             acc, count, max_radii = acc[keep], count[keep], max_radii[keep]
             info = {"n_clone": int(to_clone.sum()), "n_split": S, "stds": stds}
-    if i > 0 and i % 3000 == 0:
-        x = np.full_like(params["opacity_logits"], f32(0.01))
-        params["opacity_logits"] = np.log(x / (f32(1) - x)).astype(f32)
-        if "opacity_logits" in m:
-            m["opacity_logits"] = np.zeros_like(params["opacity_logits"])
-            v["opacity_logits"] = np.zeros_like(params["opacity_logits"])
+        if i > 0 and i % 3000 == 0:  # external.py:306-314, inside `if i <= 5000` (i = 3000 only)
+            x = np.full_like(params["opacity_logits"], f32(0.01))
+            params["opacity_logits"] = np.log(x / (f32(1) - x)).astype(f32)
+            if "opacity_logits" in m:
+                m["opacity_logits"] = np.zeros_like(params["opacity_logits"])
+                v["opacity_logits"] = np.zeros_like(params["opacity_logits"])
     return params, m, v, acc, count, max_radii, info

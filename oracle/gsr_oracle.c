@@ -165,6 +165,7 @@ void ora_preprocess(int P, int D, int M, const float *means3D, const float *scal
     const float focal_y = H / (2.0f * tan_fovy);
     const float focal_x = W / (2.0f * tan_fovx);
     const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < P; ++i) {
         radii[i] = 0;
         tiles_touched[i] = 0;
@@ -222,39 +223,51 @@ static int pair_cmp(const void *a, const void *b) {
     return x->emit < y->emit ? -1 : (x->emit > y->emit);
 }
 
-/* returns num_rendered; point_list must hold sum(tiles_touched) entries, ranges 2*T entries */
+/* returns num_rendered; point_list must hold sum(tiles_touched) entries, ranges 2*T entries.
+ * The stable sort of all K (tile << 32 | depth bits) keys is done as a stable bucketing by tile
+ * (emission order kept) followed by an independent sort of every tile's bucket by
+ * (depth bits, emission index) -- the same total order, with the tiles sorted in parallel. */
 long ora_bin(int P, const float *depths, const int *radii, const int *rects,
              const unsigned *tiles_touched, int W, int H, unsigned *point_list, unsigned *ranges) {
     const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
+    const int T = gx * gy;
     long K = 0;
     for (int i = 0; i < P; ++i) K += tiles_touched[i];
-    memset(ranges, 0, sizeof(unsigned) * 2 * (size_t)gx * gy);
+    memset(ranges, 0, sizeof(unsigned) * 2 * (size_t)T);
     if (K == 0) return 0;
     ora_pair *pairs = (ora_pair *)malloc(sizeof(ora_pair) * K);
-    long off = 0;
+    long *start = (long *)calloc((size_t)T + 1, sizeof(long));
+    for (int i = 0; i < P; ++i) {  /* tile histogram */
+        if (radii[i] <= 0) continue;
+        for (int y = rects[4 * i + 1]; y < rects[4 * i + 3]; ++y)
+            for (int x = rects[4 * i + 0]; x < rects[4 * i + 2]; ++x) ++start[y * gx + x + 1];
+    }
+    for (int t = 0; t < T; ++t) start[t + 1] += start[t];
+    long *cur = (long *)malloc(sizeof(long) * ((size_t)T + 1));
+    memcpy(cur, start, sizeof(long) * ((size_t)T + 1));
+    long off = 0;  /* emission index: Gaussian order, rect y-major then x (duplicateWithKeys) */
     for (int i = 0; i < P; ++i) {
         if (radii[i] <= 0) continue;
         uint32_t dbits;
         memcpy(&dbits, depths + i, 4);
         for (int y = rects[4 * i + 1]; y < rects[4 * i + 3]; ++y)
             for (int x = rects[4 * i + 0]; x < rects[4 * i + 2]; ++x) {
-                pairs[off].key = ((uint64_t)(y * gx + x) << 32) | dbits;
-                pairs[off].val = (uint32_t)i;
-                pairs[off].emit = (uint32_t)off;
-                ++off;
+                const int t = y * gx + x;
+                ora_pair *q = pairs + cur[t]++;
+                q->key = ((uint64_t)t << 32) | dbits;
+                q->val = (uint32_t)i;
+                q->emit = (uint32_t)off++;
             }
     }
-    qsort(pairs, K, sizeof(ora_pair), pair_cmp);
-    for (long k = 0; k < K; ++k) {
-        point_list[k] = pairs[k].val;
-        const uint32_t t = (uint32_t)(pairs[k].key >> 32);
-        if (k == 0) ranges[2 * t] = 0;
-        else {
-            const uint32_t pt = (uint32_t)(pairs[k - 1].key >> 32);
-            if (t != pt) { ranges[2 * pt + 1] = (unsigned)k; ranges[2 * t] = (unsigned)k; }
-        }
-        if (k == K - 1) ranges[2 * t + 1] = (unsigned)K;
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int t = 0; t < T; ++t) {
+        const long a = start[t], b = start[t + 1];
+        if (b > a) qsort(pairs + a, (size_t)(b - a), sizeof(ora_pair), pair_cmp);
+        for (long k = a; k < b; ++k) point_list[k] = pairs[k].val;
+        if (b > a) { ranges[2 * t] = (unsigned)a; ranges[2 * t + 1] = (unsigned)b; }
     }
+    free(cur);
+    free(start);
     free(pairs);
     return K;
 }
@@ -267,6 +280,7 @@ void ora_render(const unsigned *ranges, const unsigned *point_list, int W, int H
                 const float *bg, float *out_color, float *out_depth, float *final_T,
                 unsigned *n_contrib) {
     const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ++ty)
         for (int tx = 0; tx < gx; ++tx) {
             const unsigned r0 = ranges[2 * (ty * gx + tx)], r1 = ranges[2 * (ty * gx + tx) + 1];
@@ -301,19 +315,31 @@ void ora_render(const unsigned *ranges, const unsigned *point_list, int W, int H
 }
 
 /* ======================================================================================
- * Backward: reverse walk per pixel (SURVEY 2.1 row renderCUDA bwd).  Sums in fixed
- * (tile, pixel, back-to-front) order; the reference used float atomics (unordered).
- * dL_dmean2D is in NDC units (x 0.5W, 0.5H); dL_dconic holds (a, b/2-convention, -, c).
- * The background term enters dL/dalpha; the 0.99 clamp is ignored in the gradient.
- * Grad of the depth image is not propagated (the -w-depth reference discards it).
+ * Backward: reverse walk per pixel (SURVEY 2.1 row renderCUDA bwd).
+ * Every pixel re-walks its tile list back to front from its n_contrib, recovering the
+ * transmittance in front of each contributor by division, and forms the blend's partial
+ * derivatives.  dL/dmean2D is in NDC units (x 0.5W, 0.5H); dL/dconic holds (a, b/2-convention, -, c).
+ * The background term enters dL/dalpha; the 0.99 clamp is ignored in the gradient; the depth image
+ * carries no gradient (the -w-depth reference discards it).
+ * Summation: tiles run in parallel, each accumulating its own per-slot partials (a slot belongs to
+ * one tile) over its pixels in row-major order; the slots are then added into the per-Gaussian
+ * gradients serially in slot (tile-major) order -- fixed order, independent of the thread count.
+ * (The reference used float atomics, whose order is unspecified.)
  * ====================================================================================== */
+#define ORA_SLOT 9 /* per slot: dmean2D x,y; dconic a,b,c; dopacity; dcolour r,g,b */
 void ora_render_backward(const unsigned *ranges, const unsigned *point_list, int W, int H,
                          const float *bg, const float *xy, const float *conic_opacity,
                          const float *colors, const float *final_Ts, const unsigned *n_contrib,
                          const float *dL_dpixels, float *dL_dmean2D, float *dL_dconic,
                          float *dL_dopacity, float *dL_dcolors) {
     const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
-    const float ddelx_dx = (float)(0.5 * W), ddely_dy = (float)(0.5 * H);
+    const float ndc_sx = (float)(0.5 * W), ndc_sy = (float)(0.5 * H);
+    long K = 0;
+    for (int t = 0; t < gx * gy; ++t)
+        if ((long)ranges[2 * t + 1] > K) K = (long)ranges[2 * t + 1];
+    if (K == 0) return;
+    float *slot = (float *)calloc((size_t)K * ORA_SLOT, sizeof(float));
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
     for (int ty = 0; ty < gy; ++ty)
         for (int tx = 0; tx < gx; ++tx) {
             const unsigned r0 = ranges[2 * (ty * gx + tx)], r1 = ranges[2 * (ty * gx + tx) + 1];
@@ -321,15 +347,19 @@ void ora_render_backward(const unsigned *ranges, const unsigned *point_list, int
                 for (int px = tx * BX; px < tx * BX + BX && px < W; ++px) {
                     const int pid = py * W + px;
                     const float pfx = (float)px, pfy = (float)py;
-                    const float T_final = final_Ts[pid];
-                    float T = T_final;
-                    const unsigned last_contributor = n_contrib[pid];
-                    float accum_rec[3] = {0, 0, 0}, dL_dpixel[3], last_color[3] = {0, 0, 0};
-                    float last_alpha = 0;
-                    for (int ch = 0; ch < 3; ++ch) dL_dpixel[ch] = dL_dpixels[ch * H * W + pid];
+                    const float t_end = final_Ts[pid];
+                    float trans = t_end;
+                    const unsigned n_used = n_contrib[pid];
+                    /* colour seen behind the current contributor, and the contributor met just before
+                     * it in this back-to-front walk (its alpha and colour) */
+                    float behind[3] = {0, 0, 0}, gpix[3], prev_col[3] = {0, 0, 0};
+                    float prev_alpha = 0;
+                    for (int ch = 0; ch < 3; ++ch) gpix[ch] = dL_dpixels[ch * H * W + pid];
+                    float bg_dot = 0;
+                    for (int ch = 0; ch < 3; ++ch) bg_dot += bg[ch] * gpix[ch];
                     for (unsigned k = r1; k > r0; --k) {
-                        const unsigned pos = k - 1 - r0; /* 0-based position in tile list */
-                        if (pos >= last_contributor) continue;
+                        const unsigned pos = k - 1 - r0; /* 0-based position in the tile list */
+                        if (pos >= n_used) continue;
                         const unsigned g = point_list[k - 1];
                         const float dx = xy[2 * g] - pfx, dy = xy[2 * g + 1] - pfy;
                         const float *co = conic_opacity + 4 * g;
@@ -338,44 +368,55 @@ void ora_render_backward(const unsigned *ranges, const unsigned *point_list, int
                         const float G = expf(power);
                         const float alpha = fminf(0.99f, co[3] * G);
                         if (alpha < 1.0f / 255.0f) continue;
-                        T = T / (1.f - alpha);
-                        const float dchannel_dcolor = alpha * T;
-                        float dL_dalpha = 0.0f;
+                        trans = trans / (1.f - alpha);
+                        const float w_col = alpha * trans; /* d(pixel colour) / d(Gaussian colour) */
+                        float *o = slot + (size_t)(k - 1) * ORA_SLOT;
+                        float g_alpha = 0.0f;
                         for (int ch = 0; ch < 3; ++ch) {
                             const float c = colors[3 * g + ch];
-                            accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
-                            last_color[ch] = c;
-                            const float dL_dchannel = dL_dpixel[ch];
-                            dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
-                            dL_dcolors[3 * g + ch] += dchannel_dcolor * dL_dchannel;
+                            behind[ch] = prev_alpha * prev_col[ch] + (1.f - prev_alpha) * behind[ch];
+                            prev_col[ch] = c;
+                            g_alpha += (c - behind[ch]) * gpix[ch];
+                            o[6 + ch] += w_col * gpix[ch];
                         }
-                        dL_dalpha *= T;
-                        last_alpha = alpha;
-                        float bg_dot = 0;
-                        for (int ch = 0; ch < 3; ++ch) bg_dot += bg[ch] * dL_dpixel[ch];
-                        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                        const float dL_dG = co[3] * dL_dalpha;
+                        g_alpha *= trans;
+                        prev_alpha = alpha;
+                        g_alpha += (-t_end / (1.f - alpha)) * bg_dot;
+                        const float g_gauss = co[3] * g_alpha; /* dL/dG */
                         const float gdx = G * dx, gdy = G * dy;
-                        const float dG_ddelx = -gdx * co[0] - gdy * co[1];
-                        const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                        dL_dmean2D[3 * g + 0] += dL_dG * dG_ddelx * ddelx_dx;
-                        dL_dmean2D[3 * g + 1] += dL_dG * dG_ddely * ddely_dy;
-                        dL_dconic[4 * g + 0] += -0.5f * gdx * dx * dL_dG;
-                        dL_dconic[4 * g + 1] += -0.5f * gdx * dy * dL_dG;
-                        dL_dconic[4 * g + 3] += -0.5f * gdy * dy * dL_dG;
-                        dL_dopacity[g] += G * dL_dalpha;
+                        const float dG_dx = -gdx * co[0] - gdy * co[1];
+                        const float dG_dy = -gdy * co[2] - gdx * co[1];
+                        o[0] += g_gauss * dG_dx * ndc_sx;
+                        o[1] += g_gauss * dG_dy * ndc_sy;
+                        o[2] += -0.5f * gdx * dx * g_gauss;
+                        o[3] += -0.5f * gdx * dy * g_gauss;
+                        o[4] += -0.5f * gdy * dy * g_gauss;
+                        o[5] += G * g_alpha;
                     }
                 }
         }
+    for (long k = 0; k < K; ++k) {
+        const unsigned g = point_list[k];
+        const float *o = slot + (size_t)k * ORA_SLOT;
+        dL_dmean2D[3 * g + 0] += o[0];
+        dL_dmean2D[3 * g + 1] += o[1];
+        dL_dconic[4 * g + 0] += o[2];
+        dL_dconic[4 * g + 1] += o[3];
+        dL_dconic[4 * g + 3] += o[4];
+        dL_dopacity[g] += o[5];
+        for (int ch = 0; ch < 3; ++ch) dL_dcolors[3 * g + ch] += o[6 + ch];
+    }
+    free(slot);
 }
 
 /* ---- backward helpers ---- */
-static void dnormvdv(const float *v, const float *dv, float *o) {
-    const float sum2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-    o[0] = ((+sum2 - v[0] * v[0]) * dv[0] - v[1] * v[0] * dv[1] - v[2] * v[0] * dv[2]) * invsum32;
-    o[1] = (-v[0] * v[1] * dv[0] + (sum2 - v[1] * v[1]) * dv[1] - v[2] * v[1] * dv[2]) * invsum32;
-    o[2] = (-v[0] * v[2] * dv[0] - v[1] * v[2] * dv[1] + (sum2 - v[2] * v[2]) * dv[2]) * invsum32;
+/* Chain rule through u = v / |v|: du/dv = (|v|^2 I - v v^T) / |v|^3, applied to the gradient g. */
+static void unit_vec_bwd(const float *v, const float *g, float *o) {
+    const float n2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const float inv_n3 = 1.0f / sqrtf(n2 * n2 * n2);
+    o[0] = ((+n2 - v[0] * v[0]) * g[0] - v[1] * v[0] * g[1] - v[2] * v[0] * g[2]) * inv_n3;
+    o[1] = (-v[0] * v[1] * g[0] + (n2 - v[1] * v[1]) * g[1] - v[2] * v[1] * g[2]) * inv_n3;
+    o[2] = (-v[0] * v[2] * g[0] - v[1] * v[2] * g[1] + (n2 - v[2] * v[2]) * g[2]) * inv_n3;
 }
 
 static void sh_backward(int deg, const float *mean, const float *campos, const float *sh,
@@ -442,7 +483,7 @@ static void sh_backward(int deg, const float *mean, const float *campos, const f
                               dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
                               dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]};
     float dm[3];
-    dnormvdv(dir_orig, dL_ddir, dm);
+    unit_vec_bwd(dir_orig, dL_ddir, dm);
     dL_dmean[0] += dm[0]; dL_dmean[1] += dm[1]; dL_dmean[2] += dm[2];
 }
 
@@ -492,9 +533,10 @@ void ora_preprocess_backward(int P, int D, int M, const float *means3D, const in
     const float h_y = H / (2.0f * tan_fovy);
     const float h_x = W / (2.0f * tan_fovx);
     const float *vm = viewmatrix, *pj = projmatrix;
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < P; ++i) {
         if (!(radii[i] > 0)) continue;
-        /* ---- computeCov2DCUDA ---- */
+        /* ---- dL/dconic -> dL/dSigma2D -> dL/dSigma3D and the mean's share through J (SURVEY 2.1 computeCov2DCUDA) ---- */
         const float *c3 = cov3Ds + 6 * i;
         const float *mean = means3D + 3 * i;
         const float dcx = dL_dconic[4 * i], dcy = dL_dconic[4 * i + 1], dcz = dL_dconic[4 * i + 3];
@@ -504,8 +546,8 @@ void ora_preprocess_backward(int P, int D, int M, const float *means3D, const in
         const float txtz = t[0] / t[2], tytz = t[1] / t[2];
         t[0] = fminf(limx, fmaxf(-limx, txtz)) * t[2];
         t[1] = fminf(limy, fmaxf(-limy, tytz)) * t[2];
-        const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
-        const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+        const float keep_tx = txtz < -limx || txtz > limx ? 0 : 1;
+        const float keep_ty = tytz < -limy || tytz > limy ? 0 : 1;
         mat3 J = {{h_x / t[2], 0.0f, -(h_x * t[0]) / (t[2] * t[2]), 0.0f, h_y / t[2],
                    -(h_y * t[1]) / (t[2] * t[2]), 0, 0, 0}};
         mat3 Wm = {{vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]}};
@@ -517,12 +559,12 @@ void ora_preprocess_backward(int P, int D, int M, const float *means3D, const in
         const float a = M3(c2, 0, 0) + 0.3f, b = M3(c2, 0, 1), c = M3(c2, 1, 1) + 0.3f;
         const float denom = a * c - b * b;
         float dL_da = 0, dL_db = 0, dL_dc = 0;
-        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        const float inv_det2 = 1.0f / ((denom * denom) + 0.0000001f);
         float *dcov = dL_dcov3D + 6 * i;
-        if (denom2inv != 0) {
-            dL_da = denom2inv * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
-            dL_dc = denom2inv * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
-            dL_db = denom2inv * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
+        if (inv_det2 != 0) {
+            dL_da = inv_det2 * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
+            dL_dc = inv_det2 * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
+            dL_db = inv_det2 * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
 #define TT(cc, rr) M3(T, cc, rr)
             dcov[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
             dcov[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
@@ -558,17 +600,17 @@ void ora_preprocess_backward(int P, int D, int M, const float *means3D, const in
         const float dJ12 = WW(2, 0) * dT10 + WW(2, 1) * dT11 + WW(2, 2) * dT12;
 #undef WW
         const float tz = 1.f / t[2], tz2 = tz * tz, tz3 = tz2 * tz;
-        const float dL_dtx = x_grad_mul * -h_x * tz2 * dJ02;
-        const float dL_dty = y_grad_mul * -h_y * tz2 * dJ12;
+        const float dL_dtx = keep_tx * -h_x * tz2 * dJ02;
+        const float dL_dty = keep_ty * -h_y * tz2 * dJ12;
         const float dL_dtz = -h_x * tz2 * dJ00 - h_y * tz2 * dJ11 + (2 * h_x * t[0]) * tz3 * dJ02 +
                              (2 * h_y * t[1]) * tz3 * dJ12;
         float *dm = dL_dmeans3D + 3 * i;
-        /* transformVec4x3Transpose */
+        /* back through the view rotation: W^T (dL/dt) */
         dm[0] = vm[0] * dL_dtx + vm[1] * dL_dty + vm[2] * dL_dtz;
         dm[1] = vm[4] * dL_dtx + vm[5] * dL_dty + vm[6] * dL_dtz;
         dm[2] = vm[8] * dL_dtx + vm[9] * dL_dty + vm[10] * dL_dtz;
 
-        /* ---- preprocessCUDA backward: screen-space mean -> means3D ---- */
+        /* ---- screen-space mean -> means3D through the projection (SURVEY 2.1 preprocessCUDA bwd) ---- */
         float mh[4];
         xform4x4(mean, pj, mh);
         const float m_w = 1.0f / (mh[3] + 0.0000001f);

@@ -65,3 +65,27 @@ def test_fused_parameters_accumulate_bitwise(cuda):
     for k, v in lv.items():
         assert torch.equal(v.grad, (sep[0][0][k] + sep[1][0][k]) + sep[2][0][k]), k
     assert torch.equal(m2.grad, (sep[0][1] + sep[1][1]) + sep[2][1])
+
+
+def test_autograd_grad_and_inputs_leave_grad_alone(cuda):
+    """Stock autograd semantics: torch.autograd.grad returns the gradient and leaves .grad untouched;
+    backward(inputs=[x]) writes only x.grad.  The in-place kernel accumulation must follow them."""
+    _, base = _base(cuda, 3)
+    cams, dls = _views(cuda, 3)
+    ref = {k: v.clone().requires_grad_(True) for k, v in base.items()}
+    GaussianRasterizer(raster_settings=cams[1])(**ref)[0].backward(dls[1])
+    leaves = {k: v.clone().requires_grad_(True) for k, v in base.items()}
+    GaussianRasterizer(raster_settings=cams[0])(**leaves)[0].backward(dls[0])
+    before = {k: v.grad.clone() for k, v in leaves.items()}
+    img = GaussianRasterizer(raster_settings=cams[1])(**leaves)[0]
+    names = sorted(leaves)
+    got = torch.autograd.grad(img, [leaves[k] for k in names], dls[1])
+    for k, g in zip(names, got):
+        assert torch.equal(leaves[k].grad, before[k]), k            # .grad untouched
+        assert torch.equal(g, ref[k].grad), k                       # the gradient is returned
+    img = GaussianRasterizer(raster_settings=cams[1])(**leaves)[0]
+    img.backward(dls[1], inputs=[leaves["means3D"]])
+    assert torch.equal(leaves["means3D"].grad, before["means3D"] + ref["means3D"].grad)
+    for k in names:
+        if k != "means3D":
+            assert torch.equal(leaves[k].grad, before[k]), k

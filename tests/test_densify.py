@@ -233,3 +233,40 @@ def test_gpu_densify_off_schedule_and_empty(cuda):
     pr = 1 / (1 + np.exp(-g["opacity_logits"][:, 0])) < np.float32(0.005)
     np.testing.assert_array_equal(params["colors"].detach().cpu().numpy(), g["colors"][~pr])
     assert float(dv.visibility_count.abs().sum()) == 0 and dv.visibility_count.numel() == int((~pr).sum())
+
+
+def test_oracle_opacity_reset_only_at_3000():
+    """external.py:306-314 sits inside `if i <= 5000:` (external.py:218): the opacity reset fires at
+    i = 3000 and never again (i = 6000, 9000, ... leave opacity_logits and its moments alone)."""
+    keys, g, m, v = _case(0)
+    P = g["means"].shape[0]
+    z = np.zeros(P, np.float32)
+    for i, resets in ((3000, True), (6000, False), (9000, False), (27000, False)):
+        p2, m2, v2, *_ = DO.densify(g, m, v, z, z, z, np.zeros(P, bool), np.zeros((P, 3), np.float32), 2.0, i,
+                                    np.zeros((0, 3), np.float32))
+        if resets:
+            assert np.allclose(1 / (1 + np.exp(-p2["opacity_logits"])), 0.01, atol=1e-6)
+            assert not m2["opacity_logits"].any()
+        else:
+            np.testing.assert_array_equal(p2["opacity_logits"], g["opacity_logits"])
+            np.testing.assert_array_equal(m2["opacity_logits"], m["opacity_logits"])
+            np.testing.assert_array_equal(v2["opacity_logits"], v["opacity_logits"])
+
+
+@pytest.mark.gpu
+def test_gpu_opacity_reset_only_at_3000(cuda):
+    import splat_densify
+    keys, g, m, v = _case(0)
+    P = g["means"].shape[0]
+    for i, resets in ((6000, False), (9000, False), (3000, True)):
+        params, opt = _gpu_setup(cuda, keys, g, m, v)
+        dv = _dv(cuda, np.zeros(P, np.float32), np.zeros(P, np.float32), np.zeros(P, np.float32),
+                 np.zeros(P, bool), np.zeros((P, 3), np.float32))
+        splat_densify.densify_gaussians(params, dv, 2.0, opt, i)
+        ol = params["opacity_logits"].detach().cpu().numpy()
+        st = opt.state[params["opacity_logits"]]
+        if resets:
+            assert np.allclose(1 / (1 + np.exp(-ol)), 0.01, atol=1e-6) and not st["exp_avg"].any()
+        else:
+            np.testing.assert_array_equal(ol, g["opacity_logits"])
+            np.testing.assert_array_equal(st["exp_avg"].cpu().numpy(), m["opacity_logits"])

@@ -67,7 +67,7 @@ def test_grad_fence_orders_a_reset_before_the_next_backward(cuda):
     main.wait_stream(s1)
     for v in leaves.values():  # the "all-reduce + reset" on the main stream ...
         v.grad.mul_(3.0).zero_()
-    _C.grad_fence(leaves["means3D"].grad)  # ... declared to the library
+    _C.grad_fence(*[v.grad for v in leaves.values()])  # ... declared to the library
     with torch.cuda.stream(s2):  # second view, other stream: accumulates into the reset gradients
         GaussianRasterizer(raster_settings=cam)(**leaves)[0].backward(dl)
     torch.cuda.synchronize()
@@ -76,3 +76,44 @@ def test_grad_fence_orders_a_reset_before_the_next_backward(cuda):
     torch.cuda.synchronize()
     for k in ref:
         assert torch.equal(leaves[k].grad, ref[k].grad), k
+
+
+def test_multistream_without_means3d_grad_and_many_sets(cuda):
+    """Ordering is per gradient array, not per set: with means3D frozen (a fresh, never-accumulated
+    means3D gradient each call) the colour / opacity / scale / rotation accumulations across two
+    streams must still be ordered, and 20 gradient sets in flight (more than any fixed table) must
+    not drop a pending writer."""
+    P, W, H = 20_000, 256, 192
+    p = S.synthetic_cloud(P, 0.01, sh_degree=-1, seed=8, device=cuda)
+    a = S.activated_inputs(p, -1)
+    cams = [S.render_settings(W, H, S.intrinsics(240.0, W, H), S.look_at(yaw, 0.2, 4), device=cuda)
+            for yaw in (0, 30, 60, 90)]
+    dl = S.upstream_grad(H, W, device=cuda)
+    nsets = 20
+
+    def make():
+        lv = [{k: v.detach().clone().requires_grad_(k != "means3D") for k, v in a.items()} for _ in range(nsets)]
+        return lv
+
+    def run(n):
+        sets = make()
+        main = torch.cuda.current_stream()
+        streams = [main] + [torch.cuda.Stream() for _ in range(n - 1)]
+        for s in streams[1:]:
+            s.wait_stream(main)
+        k = 0
+        for cam in cams:
+            for lv in sets:
+                with torch.cuda.stream(streams[k % n]):
+                    GaussianRasterizer(raster_settings=cam)(**lv)[0].backward(dl)
+                k += 1
+        for s in streams[1:]:
+            main.wait_stream(s)
+        torch.cuda.synchronize()
+        return [{kk: v.grad.clone() for kk, v in lv.items() if v.grad is not None} for lv in sets]
+
+    g1, g2 = run(1), run(2)
+    for x, y in zip(g1, g2):
+        assert set(x) == set(y) and "means3D" not in x
+        for kk in x:
+            assert torch.equal(x[kk], y[kk]), kk

@@ -1,5 +1,5 @@
 """One densify.py iteration on the native path (splat_train.densify_iteration) vs the reference's
-composition of the same step (densify.py:110-162,234-258): torch activations (shared.py:29-42) +
+composition of the same step (densify.py:110-162,218-247): torch activations (shared.py:29-42) +
 GaussianRasterizer + 0.8 l1 + 0.2 (1 - calc_ssim) (restated with torch ops, the reference's
 external.py:68-110) + torch statistics + torch.optim.Adam.
 
