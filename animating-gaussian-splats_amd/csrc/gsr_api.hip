@@ -216,10 +216,10 @@ void carve_geom(FwdArgs &a, char *base) {
 }
 void carve_image(FwdArgs &a, char *base) {
     const ImageLayout L(a.W, a.H, a.P);
-    a.ranges = (uint2 *)(base + L.ranges); a.final_T = (float *)(base + L.final_T);
+    a.ranges = (uint2 *)(base + L.ranges); a.pix_end = (float4 *)(base + L.pix_end);
     a.n_contrib = (uint32_t *)(base + L.n_contrib); a.tile_maxc = (uint32_t *)(base + L.tile_maxc);
     a.tile_order_f = (uint32_t *)(base + L.tile_order_f);
-    a.tile_order_b = (uint32_t *)(base + L.tile_order_b);
+    a.seg_off = (uint32_t *)(base + L.seg_off);
     a.sort_lists = (uint32_t *)(base + L.sort_lists);
     a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
     a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
@@ -230,6 +230,7 @@ void carve_binning(FwdArgs &a, char *base, int K) {
     a.pairs = (uint4 *)(base + L.pairs);
     a.point_list = (uint32_t *)(base + L.point_list);
     a.slot_emit = (uint32_t *)(base + L.slot_emit);
+    a.seg_state = (float4 *)(base + L.seg_state);
 }
 
 }  // namespace
@@ -242,17 +243,19 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 size_t gsr_geom_bytes(int P) { return GeomLayout(P < 0 ? 0 : P).total; }
 size_t gsr_image_bytes(int W, int H, int P) { return ImageLayout(W, H, P < 0 ? 0 : P).total; }
 size_t gsr_binning_bytes(int K) { return BinningLayout(K).total; }
-size_t gsr_scratch_bytes(int K) { return ScratchLayout(K).total; }
+size_t gsr_scratch_bytes(int K, int W, int H) {
+    return ScratchLayout(K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH)).total;
+}
 
 int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const GeomLayout g(P);
     const ImageLayout im(W, H, P);
     const BinningLayout b(K);
-    const size_t v[12] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
-                          im.ranges, im.final_T, im.n_contrib, im.tile_maxc,
-                          b.pairs, b.point_list, b.slot_emit};
+    const size_t v[14] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
+                          im.ranges, im.pix_end, im.n_contrib, im.tile_maxc,
+                          b.pairs, b.point_list, b.slot_emit, im.seg_off, b.seg_state};
     int n = 0;
-    for (; n < 12 && n < max_out; ++n) out[n] = v[n];
+    for (; n < 14 && n < max_out; ++n) out[n] = v[n];
     return n;
 }
 
@@ -353,20 +356,22 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.viewmatrix = f.viewmatrix; a.projmatrix = f.projmatrix; a.campos = f.campos; a.bg = f.bg; a.cs = f.cs;
     a.radii = radii;
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff;
-    a.ranges = f.ranges; a.final_T = f.final_T; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
-    a.tile_order_b = f.tile_order_b;
-    a.point_list = f.point_list; a.slot_emit = f.slot_emit;
+    a.ranges = f.ranges; a.pix_end = f.pix_end; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
+    a.seg_off = f.seg_off; a.meta = f.meta;
+    a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
     a.dL_dcolor = dL_dcolor;
     a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
     a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = out->dL_dsh;
     a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
     if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward: unknown accumulate bits 0x%x", out->accumulate);
     a.accm = out->accumulate;
-    char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, ScratchLayout(num_rendered).total);
+    const ScratchLayout SL(num_rendered, a.gx * a.gy);
+    char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, SL.total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
-    const ScratchLayout SL(num_rendered);
     a.part = (float4 *)(scr + SL.part);
-    { Phase ph(s, "tile_order_bwd"); HIP_TRY(launch_tile_order_bwd(a, s)); }
+    a.items = (uint2 *)(scr + SL.items);
+    a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
+    { Phase ph(s, "bwd_items"); HIP_TRY(launch_bwd_items(a, s)); }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
     const void *written[8] = {a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity, a.dL_dmeans3D,
                               a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot};

@@ -1,11 +1,11 @@
 // gsr_backward.hip -- backward pass of the MI355X-native Gaussian-splat rasterizer.
 //
-//   k_render_bwd  1 block (4 wave64) / 16x16 tile: per-pixel reverse walk (SURVEY.md 2.1 row
-//                 renderCUDA bwd).  Instead of the reference's per-pixel float atomics into
-//                 per-Gaussian buffers, every wave reduces its 64 pixels' 9 partials with DPP,
-//                 the 4 wave sums are added in fixed order, and one 36-byte record per sorted
-//                 (tile, Gaussian) slot is stored with plain coalesced stores: no global atomics,
-//                 bitwise reproducible.
+//   k_render_bwd  1 wave64 / (tile, segment of kSeg entries): per-pixel reverse walk (SURVEY.md 2.1
+//                 row renderCUDA bwd) from the blend state the forward saved at the segment's end.
+//                 Instead of the reference's per-pixel float atomics into per-Gaussian buffers, the
+//                 wave reduces its 256 pixels' partials with permlane swaps + DPP and stores one
+//                 36-byte record per (tile, Gaussian) pair at the pair's emission slot: no global
+//                 atomics, bitwise reproducible.
 //   k_gauss_bwd   1 thread / Gaussian: sums its slot records in emission order (through the
 //                 emission->slot map written by k_tile_sort), then the fused per-Gaussian chain
 //                 computeCov2D bwd -> projection bwd -> SH bwd -> Sigma3D bwd (SURVEY.md 2.1 rows
@@ -21,61 +21,95 @@ namespace gsr {
 __device__ uint64_t *g_trace_bwd;
 #endif
 
-// Backward dispatch order (one block): tiles by descending sum of their quarters' max n_contrib (the
-// pairs each quarter walks: the per-pair evaluations and reductions follow it far more closely than
-// the sum of n_contrib over the pixels), laid out boustrophedon over rounds of one wave per SIMD.
-__global__ __launch_bounds__(1024) void k_tile_order_bwd(int T, const uint32_t *__restrict__ tile_maxc,
-                                                         uint32_t *__restrict__ tile_order, int simds) {
-    const SnakePos pos{(uint32_t)max(simds, 1), (uint32_t)T};
-    __shared__ uint32_t s_red[16];
+// The backward's work items in longest-first order, built by one block from the forward's tile
+// ranges and per-quarter maxima: items bucketed by exact cost (bwd_item_cost + a fixed per-item
+// start-up cost, kOrderBuckets buckets, descending), so the hardware's in-order dispatch of the
+// launch's residency rounds is a greedy LPT schedule.  Item order inside a bucket follows LDS
+// atomics (scheduling only: every item writes its own slots).  items[0].x = the item count.
+constexpr uint32_t kItemStartCost = 64;  // init loads + first gathers, in (pair, quarter) steps
+__global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restrict__ ranges,
+                                                    const uint32_t *__restrict__ tile_maxc,
+                                                    uint2 *__restrict__ items) {
     __shared__ uint32_t s_hist[kOrderBuckets];
-    if (T <= kScanRegs * (int)blockDim.x) {  // costs prefetched into registers, all loads in flight
-        const int c = div_up(T, (int)blockDim.x), t0 = threadIdx.x * c;
-        uint32_t cost[kScanRegs];
+    __shared__ uint32_t s_red[16];
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
+    constexpr uint32_t kMaxCost = 4u * kSeg + kItemStartCost;
+    constexpr uint32_t kShift = kMaxCost >= (uint32_t)kOrderBuckets ? 32 - __builtin_clz(kMaxCost / kOrderBuckets) : 0;
+    auto bucket = [](uint32_t cost) { return (uint32_t)kOrderBuckets - 1u - min(cost >> kShift, (uint32_t)kOrderBuckets - 1u); };
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int t0 = 0; t0 < T; t0 += kScanRegs * (int)blockDim.x) {  // kScanRegs tiles' loads in flight
+            uint32_t nn[kScanRegs];
+            uint4 mq[kScanRegs];
 #pragma unroll
-        for (int i = 0; i < kScanRegs; ++i) {
-            uint4 q = make_uint4(0, 0, 0, 0);
-            if (i < c && t0 + i < T) q = reinterpret_cast<const uint4 *>(tile_maxc)[t0 + i];
-            cost[i] = q.x + q.y + q.z + q.w;
+            for (int i = 0; i < kScanRegs; ++i) {
+                const int t = t0 + i * (int)blockDim.x + (int)threadIdx.x;
+                const uint2 rg = t < T ? ranges[t] : make_uint2(0, 0);
+                mq[i] = t < T ? reinterpret_cast<const uint4 *>(tile_maxc)[t] : make_uint4(0, 0, 0, 0);
+                nn[i] = rg.y - rg.x;
+            }
+#pragma unroll
+            for (int i = 0; i < kScanRegs; ++i) {
+                const uint32_t t = (uint32_t)(t0 + i * (int)blockDim.x + (int)threadIdx.x);
+                const uint32_t J = bwd_item_count(nn[i], mq[i]);
+                for (uint32_t j = 0; j < J; ++j) {
+                    const uint32_t b = bucket(bwd_item_cost(j, mq[i]) + kItemStartCost);
+                    if (pass == 0) atomicAdd(&s_hist[b], 1u);
+                    else items[1 + atomicAdd(&s_hist[b], 1u)] = make_uint2(t, j);
+                }
+            }
         }
-        lpt_order_regs<kScanRegs>(T, c, cost, tile_order, s_hist, s_red, pos);
-        return;
+        if (pass == 0) {
+            __syncthreads();
+            uint32_t carry = 0;
+            for (int base = 0; base < kOrderBuckets; base += blockDim.x) {
+                const int b = base + threadIdx.x;
+                const uint32_t h = b < kOrderBuckets ? s_hist[b] : 0;
+                uint32_t tot;
+                const uint32_t ex = block_excl_scan_u32(h, s_red, &tot) + carry;
+                if (b < kOrderBuckets) s_hist[b] = ex;
+                carry += tot;
+            }
+            if (threadIdx.x == 0) items[0] = make_uint2(carry, 0u);
+            __syncthreads();
+        }
     }
-    lpt_order(T, [&](int t) {
-        const uint4 c = reinterpret_cast<const uint4 *>(tile_maxc)[t];
-        return c.x + c.y + c.z + c.w;
-    }, tile_order, s_hist, s_red, pos);
 }
 
-// One wave64 per tile, 4 pixels per lane, reverse walk over the tile's list in batches of 64;
-// 4 independent tiles per 256-thread block, dispatched by descending work (tile_order).
-// Per surviving (tile, Gaussian) pair each contributing pixel adds s = dL/dG * G times
-// (dx, dy, dx^2, dx dy, dy^2) plus dL/dopacity and dL/dcolour terms; the lane sums its 4 pixels
-// in registers, the wave reduces them with permlane swaps + DPP (wave_pair_sums), and at the end of
-// the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
-// quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour)
-// with the exact conic, storing one 36-byte record per sorted slot (coalesced, no atomics).
-__device__ __forceinline__ void render_bwd_tile(
-    int t_lin, int W, int H, int gx, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
+// One wave64 per (tile, segment) item, 4 pixels per lane (pixel k of lane l: column l & 15, row
+// (l >> 4) + 4 k, i.e. quarter k = rows 4k..4k+3), reverse walk over the segment's entries in
+// batches of 64.  Per surviving (tile, Gaussian) pair each contributing pixel adds s = dL/dG * G
+// times (dx, dy, dx^2, dx dy, dy^2) plus dL/dopacity and dL/dcolour terms; the lane sums its 4
+// pixels in registers, the wave reduces them with permlane swaps + DPP (wave_pair_sums), and at the
+// end of the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
+// quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour) with
+// the exact conic, storing one 36-byte record at the pair's emission slot (no atomics).
+//
+// A segment [s0, s0 + kSeg) starts from the blend state behind its last entry: for a quarter whose
+// pixels' contributors reach past the segment, the state the forward saved at that boundary --
+// transmittance T and front colour C_f, so the colour behind, projected on dL/dpixel, is
+// AR = (<dL/dpix, C_all - C_f> + T_final <bg, dL/dpix>) / T -- otherwise the pixel's final state
+// (T_final, AR = <bg, dL/dpix>).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_render_bwd(
+    int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
-    const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
+    const float4 *__restrict__ rec, const float *__restrict__ bg, const float4 *__restrict__ pix_end,
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
+    const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
-    float4 *__restrict__ part, float4 (&s_rec)[kTilesPerBlock][3][64],
-    float (&s_outs)[kTilesPerBlock][64 * kPartial]) {
-    const int wv = threadIdx.x >> 6;
+    float4 *__restrict__ part) {
+    __shared__ float4 s_a[64], s_b[64], s_c[64];
+    __shared__ float s_out[64 * kPartial];  // per staged pair: its kPartial wave sums
+    if (blockIdx.x >= items[0].x) return;  // the launch covers the item bound
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t tr_evals = 0, tr_reds = 0;  // (pair, quarter) evaluations and wave reductions
 #endif
-    float4(&s_a)[64] = s_rec[wv][0];
-    float4(&s_b)[64] = s_rec[wv][1];
-    float4(&s_c)[64] = s_rec[wv][2];
-    float *s_out = s_outs[wv];
-    const int tile = (int)tile_order[t_lin];
+    const uint2 it = items[1 + blockIdx.x];
+    const int tile = (int)it.x;
+    const uint32_t seg = it.y;
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    if (n <= 0) return;
     const int tx = tile % gx, ty = tile / gx;
     const int lane = threadIdx.x & 63;
     const int px = tx * kTileW + (lane & 15);
@@ -85,76 +119,91 @@ __device__ __forceinline__ void render_bwd_tile(
     const float tx1 = tx0 + (kTileW - 1);
     const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
     const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
-    for (int p = maxc + lane; p < n; p += 64) {  // slots nobody reached: zero records
-        float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
-        dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int s0 = (int)seg * kSeg, s1f = s0 + kSeg;
+    const int s1 = min(s1f, maxc);
+    if (s1f >= maxc) {  // the tile's last item: slots nobody reached get zero records
+        for (int p = maxc + lane; p < n; p += 64) {
+            float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
+            dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dst[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
     const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     // Per pixel state of the reverse walk.  The reference keeps accum_rec and last_color per channel
     // and folds the previous contributor into accum_rec when it meets the next one; dL/dalpha only
     // needs the projection of accum_rec on dL/dpixel, and folding eagerly right after each
-    // contributor (AR <- AR + alpha (<c, dL/dpix> - AR)) gives the same value with the same
-    // rounding, while a non-contributing pair (alpha = 0) leaves it untouched without a select.
-    // The reference's background term -T_final / (1 - alpha) <bg, dL/dpix> is carried inside AR:
-    // starting the recurrence at AR = <bg, dL/dpix> (the background seen through T_final) gives
-    // exactly T_before * (<c, dL/dpix> - AR) = reference dL/dalpha, with no per-pair bg term.
+    // contributor (AR <- AR + alpha (<c, dL/dpix> - AR)) gives the same value, while a
+    // non-contributing pair (alpha = 0) leaves it untouched without a select.  The reference's
+    // background term -T_final / (1 - alpha) <bg, dL/dpix> is carried inside AR: starting the
+    // recurrence from the background seen through T_final gives exactly T_before (<c, dL/dpix> - AR).
     float Tt[4], dp0[4], dp1[4], dp2[4], AR[4], pfy[4];
     uint32_t lastc[4];
+    const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
+    const bool has_bound = s1f < n;
+    const size_t bidx = has_bound ? ((size_t)seg_off[tile] + seg) * kTilePix : 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int py = py0 + 4 * k;
         pfy[k] = (float)py;
         const bool inside = px < W && py < H;
         const int pid = py * W + px;
-        const float Tf = inside ? final_Ts[pid] : 0.f;
-        Tt[k] = Tf;
+        const float4 pe = inside ? pix_end[pid] : make_float4(0.f, 0.f, 0.f, 0.f);
         lastc[k] = inside ? n_contrib[pid] : 0u;
         dp0[k] = inside ? dL_dpixels[pid] : 0.f;
         dp1[k] = inside ? dL_dpixels[H * W + pid] : 0.f;
         dp2[k] = inside ? dL_dpixels[2 * H * W + pid] : 0.f;
         float bd = 0;
         bd += bg0 * dp0[k]; bd += bg1 * dp1[k]; bd += bg2 * dp2[k];
-        AR[k] = bd;
+        if (has_bound && qmax[k] >= (uint32_t)s1f) {  // wave-uniform: this quarter resumes at the boundary
+            const float4 st = seg_state[bidx + 64 * k + lane];
+            Tt[k] = st.w;
+            const float behind = dp0[k] * (pe.x - st.x) + dp1[k] * (pe.y - st.y) + dp2[k] * (pe.z - st.z);
+            AR[k] = st.w > 0.f ? (behind + pe.w * bd) / st.w : bd;
+        } else {
+            Tt[k] = pe.w;
+            AR[k] = bd;
+        }
     }
     const int row = lane >> 4;
     // s_out slots per pair: 0 sum dx S0, 1 sum S1, 2 sum dx^2 S0, 3 sum dx S1, 4 sum S4, 5 sum S0,
     // 6..8 sum cs (the first five still to be scaled by the opacity); wave_pair_sums row map:
     const int xslot = (row == 0) ? 0 : (row == 1) ? 4 : (row == 2) ? 1 : 6;
     const int yslot = (row == 0) ? 2 : (row == 1) ? 7 : (row == 2) ? 3 : 8;
-    // the batch ending at `e` (slots [max(e - 64, 0), e)): lane j's slot, its Gaussian's whole render
+    // the batch ending at `e` (slots [max(e - 64, s0), e)): lane j's slot, its Gaussian's whole render
     // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
     // behind the current batch's pairs
-    float4 a_n = make_float4(0.f, 0.f, 0.f, 0.f), b_n = a_n, c_n = a_n, cj_n = a_n;
-    uint32_t em_n = 0;
+    // the point list entry of each batch's slot is loaded one batch ahead (the render record gathers
+    // depend on it); the records themselves are gathered at the batch start
+    uint32_t g_n = 0, em_n = 0;
     auto fetch = [&](int e) {
-        const int st = e > 64 ? e - 64 : 0;
+        const int st = e - 64 > s0 ? e - 64 : s0;
         if (lane < e - st) {
-            const uint32_t g = point_list[rg.x + st + lane];
+            g_n = point_list[rg.x + st + lane];
             em_n = slot_emit[rg.x + st + lane];
-            a_n = rec[(size_t)kRecF4 * g]; b_n = rec[(size_t)kRecF4 * g + 1];
-            c_n = rec[(size_t)kRecF4 * g + 2]; cj_n = rec[(size_t)kRecF4 * g + 3];
         }
     };
-    if (maxc > 0) fetch(maxc);
-    for (int end = maxc; end > 0; end -= 64) {
-        const int start = end > 64 ? end - 64 : 0;
+    if (s1 > s0) fetch(s1);
+    for (int end = s1; end > s0; end -= 64) {
+        const int start = end - 64 > s0 ? end - 64 : s0;
         const int cnt = end - start;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, cj = a;
+        const uint32_t em = em_n;
+        if (lane < cnt) {
+            const float4 *r = rec + (size_t)kRecF4 * g_n;
+            a = r[0]; b = r[1]; c = r[2]; cj = r[3];  // cj: exact conic (a, b, c) of the staged Gaussian
+        }
+        if (end - 64 > s0) fetch(end - 64);
 #pragma unroll
         for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
         // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile; a
         // quarter whose pixels all precede this slot in the forward's order (p >= its max
         // n_contrib) is skipped too
         uint32_t qmask = 0;
-        const float4 cj = cj_n;  // exact conic (a, b, c) of the Gaussian this lane stages
-        const uint32_t em = em_n;
         if (lane < cnt) {
             const uint32_t p = (uint32_t)(start + lane);
-            const float4 a = a_n, b = b_n, c = c_n;
             s_a[lane] = a; s_b[lane] = b;
-            const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (p < qmax[k] &&
@@ -162,14 +211,26 @@ __device__ __forceinline__ void render_bwd_tile(
                     qmask |= 1u << k;
             s_c[lane] = make_float4(c.x, c.y, c.z, __uint_as_float(qmask));  // .w: the quarter mask
         }
-        if (end > 64) fetch(end - 64);
         uint64_t m = __ballot(qmask != 0);
         wave_lds_sync();
+#if GSR_BWD_PREFETCH
+        // the next pair's staged records are read from LDS while this pair is evaluated
+        int jn = m ? 63 - __builtin_clzll(m) : -1;
+        float4 an = make_float4(0.f, 0.f, 0.f, 0.f), bn = an, cn = an;
+        if (jn >= 0) { an = s_a[jn]; bn = s_b[jn]; cn = s_c[jn]; }
+        while (jn >= 0) {
+            const int j = jn;
+            m &= ~(1ull << j);
+            const float4 a = an, b = bn, c = cn;
+            jn = m ? 63 - __builtin_clzll(m) : -1;
+            if (jn >= 0) { an = s_a[jn]; bn = s_b[jn]; cn = s_c[jn]; }
+#else
         while (m) {
             const int j = 63 - __builtin_clzll(m);
             m &= ~(1ull << j);
-            const uint32_t p = (uint32_t)(start + j);
             const float4 a = s_a[j], b = s_b[j], c = s_c[j];
+#endif
+            const uint32_t p = (uint32_t)(start + j);
             const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));  // wave-uniform quarter mask
             const PairX x = pair_x(a, pfx);
             // per-lane sums over this lane's pixels: S0 = sum G dL/dalpha, S1 = sum G dL/dalpha dy,
@@ -239,26 +300,8 @@ __device__ __forceinline__ void render_bwd_tile(
         }
     }
 #ifdef GSR_TRACE
-    trace_wave(g_trace_bwd, t_lin, t_start, tr_evals | ((uint64_t)tr_reds << 32));
+    trace_wave(g_trace_bwd, blockIdx.x, t_start, tr_evals | ((uint64_t)tr_reds << 32));
 #endif
-}
-
-// One wave per tile, 4 tiles per block, every wave resident at once on MI355X (<= 6144 slots): the
-// order (k_tile_order_bwd) decides which SIMD holds which tiles, so it is an LPT list laid out
-// boustrophedon over rounds of one wave per SIMD (SnakePos) to even out each SIMD's total.
-__global__ __launch_bounds__(256) void k_render_bwd(
-    int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
-    const uint32_t *__restrict__ point_list,
-    const float4 *__restrict__ rec, const float *__restrict__ bg, const float *__restrict__ final_Ts,
-    const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
-    const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
-    float4 *__restrict__ part) {
-    __shared__ float4 s_rec[kTilesPerBlock][3][64];
-    __shared__ float s_outs[kTilesPerBlock][64 * kPartial];  // per staged pair: its kPartial wave sums
-    const int t_lin = (int)blockIdx.x * kTilesPerBlock + (int)(threadIdx.x >> 6);
-    if (t_lin < T)
-        render_bwd_tile(t_lin, W, H, gx, tile_order, ranges, point_list, rec, bg, final_Ts, n_contrib,
-                        tile_maxc, slot_emit, dL_dpixels, part, s_rec, s_outs);
 }
 
 // Gradient output write: plain store, or (accumulate bit set, gsr_grads.accumulate) add into the
@@ -681,30 +724,18 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 
 
 // ==========================================================================================
-// SIMDs of the current device (CUs x 4), cached per device: the round size of the backward's order.
-static int device_simds() {
-    static int cache[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
-    if (!cache[dev]) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-        cache[dev] = 4 * cus;
-    }
-    return cache[dev];
-}
-
-hipError_t launch_tile_order_bwd(const BwdArgs &a, hipStream_t s) {
+hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
     if (a.K == 0) return hipSuccess;
-    k_tile_order_bwd<<<1, 1024, 0, s>>>(a.gx * a.gy, a.tile_maxc, a.tile_order_b, device_simds());
+    k_bwd_items<<<1, 1024, 0, s>>>(a.gx * a.gy, a.ranges, a.tile_maxc, a.items);
     return hipGetLastError();
 }
 
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
-    const int T = a.gx * a.gy;
     if (a.K == 0) return hipSuccess;
-    k_render_bwd<<<div_up(T, kTilesPerBlock), 64 * kTilesPerBlock, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_b, a.ranges, a.point_list, a.rec, a.bg, a.final_T,
-                                  a.n_contrib, a.tile_maxc, a.slot_emit, a.dL_dcolor, a.part);
+    // one wave per item; the launch covers the item bound, waves without an item exit at once
+    k_render_bwd<<<a.max_items, 64, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
+                                             a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
+                                             a.slot_emit, a.dL_dcolor, a.part);
     return hipGetLastError();
 }
 

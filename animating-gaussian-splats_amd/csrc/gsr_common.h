@@ -64,9 +64,45 @@ struct BinGrid {
     }
 };
 
+// Backward segments: the backward blend walks each tile's list in independent work items of up to
+// kSeg list entries (SURVEY.md 2.1 renderCUDA bwd restated as (tile, segment) items, so a long list
+// spreads over several waves and no item costs more than 4 kSeg (pair, quarter) steps -- a
+// longest-first dispatch then balances the launch).  The forward saves every pixel's blend state
+// (front colour, transmittance) before entry kSeg, 2 kSeg, ... of its tile: the state a segment's
+// reverse walk starts from.  A power of two >= the forward's 64-entry batch (k_render_fwd tests
+// boundaries with a mask).  256: measured against 128 / 512 / 1024 (tools/ab_variants.sh).
+#ifndef GSR_KSEG
+#define GSR_KSEG 256
+#endif
+constexpr int kSeg = GSR_KSEG;
+static_assert(kSeg >= 64 && (kSeg & (kSeg - 1)) == 0, "kSeg: a power of two, >= the forward's 64-entry batch");
+__host__ __device__ inline uint32_t seg_bounds(uint32_t n) { return n > 0 ? (n - 1) / kSeg : 0; }
+
+// The backward's work items of a tile with n list entries and per-quarter max n_contrib mq: one per
+// kSeg entries below the largest quarter maximum (at least one per non-empty tile, which also
+// writes the zero records of the entries nobody reached); cost = its (pair, quarter) steps.
+__host__ __device__ inline uint32_t bwd_item_count(uint32_t n, uint4 mq) {
+    const uint32_t maxc = min(max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
+    return n == 0 ? 0u : max(1u, (maxc + kSeg - 1) / kSeg);
+}
+__host__ __device__ inline uint32_t bwd_item_cost(uint32_t j, uint4 mq) {
+    const uint32_t s0 = j * kSeg, s1 = s0 + kSeg;
+    const uint32_t a = mq.x > s0 ? min(mq.x, s1) - s0 : 0u, b = mq.y > s0 ? min(mq.y, s1) - s0 : 0u;
+    const uint32_t c = mq.z > s0 ? min(mq.z, s1) - s0 : 0u, d = mq.w > s0 ? min(mq.w, s1) - s0 : 0u;
+    return a + b + c + d;
+}
+// the upper bound of the item count the backward launch covers
+__host__ __device__ inline size_t max_bwd_items(int K, int T) {
+    const size_t k = (size_t)(K > 0 ? K : 0);
+    return k / kSeg + (k < (size_t)T ? k : (size_t)T) + 1;
+}
+
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
+//   pix_end: per pixel (C0, C1, C2, T) at the end of the blend (accumulated colour without the
+//            background, final transmittance);  seg_off: per tile, exclusive prefix of its interior
+//            segment boundaries (seg_bounds) -> index of its first saved boundary state.
 struct ImageLayout {
-    size_t ranges, final_T, n_contrib, tile_maxc, tile_order_f, tile_order_b, sort_lists,
+    size_t ranges, pix_end, n_contrib, tile_maxc, tile_order_f, seg_off, sort_lists,
         tile_count, tile_cursor, block_sums, block_off, meta, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
@@ -74,11 +110,11 @@ struct ImageLayout {
         const int NB = BinGrid(P).NB;
         size_t o = 0;
         ranges = o;      o = align256(o + sizeof(uint2) * T);
-        final_T = o;     o = align256(o + sizeof(float) * N);
+        pix_end = o;     o = align256(o + sizeof(float4) * N);
         n_contrib = o;   o = align256(o + sizeof(uint32_t) * N);
         tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter tile (16x4 px)
         tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
-        tile_order_b = o; o = align256(o + sizeof(uint32_t) * T);    // backward dispatch order (LPT)
+        seg_off = o;     o = align256(o + sizeof(uint32_t) * (T + 1));
         sort_lists = o;  o = align256(o + sizeof(uint32_t) * T);      // tiles longer than kFwdSortCap
         tile_count = o;  o = align256(o + sizeof(uint32_t) * T);
         tile_cursor = o; o = align256(o + sizeof(uint32_t) * T);
@@ -90,9 +126,11 @@ struct ImageLayout {
 };
 
 // BINNING (per Gaussian-tile pair, K): sort keys + their emission index, sorted Gaussian list,
-// emission index of every sorted slot (where the backward stores the slot's gradient record).
+// emission index of every sorted slot (where the backward stores the slot's gradient record), the
+// saved blend state at every interior segment boundary (<= K / kSeg boundaries in total; each 256
+// float4 (C0, C1, C2, T), one per pixel of the tile in row-major order).
 struct BinningLayout {
-    size_t pairs, point_list, slot_emit, total;
+    size_t pairs, point_list, slot_emit, seg_state, total;
     __host__ __device__ BinningLayout(int K) {
         size_t o = 0;
         // one 16-byte record per pair: (index, depth bits, emission index, 0) -- the 64-bit sort key
@@ -101,6 +139,7 @@ struct BinningLayout {
         pairs = o;      o = align256(o + sizeof(uint4) * (K > 0 ? K : 1));
         point_list = o; o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
         slot_emit = o;  o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));  // sorted slot -> emission
+        seg_state = o;  o = align256(o + sizeof(float4) * kTilePix * (size_t)(K / kSeg + 1));
         total = o;
     }
 };
@@ -108,13 +147,16 @@ struct BinningLayout {
 // SCRATCH (backward): one 48-byte partial-gradient record per Gaussian-tile pair, stored at the
 // pair's EMISSION index (Gaussian-major), so each Gaussian's records are contiguous for the
 // per-Gaussian reduction: (dmean2D.xy, dconic.a, dconic.b) (dconic.c, dopacity, dcolour.rg)
-// (dcolour.b, -, -, -).
+// (dcolour.b, -, -, -); then the backward's work items ([0].x = count, then (tile, segment) in
+// dispatch order, built by k_bwd_items).
 struct ScratchLayout {
-    size_t part, total;
-    __host__ __device__ ScratchLayout(int K) {
+    size_t part, items, total;
+    __host__ __device__ ScratchLayout(int K, int T) {
         const size_t k = size_t(K > 0 ? K : 1);
-        part = 0;
-        total = align256(sizeof(float4) * 3 * k);
+        size_t o = 0;
+        part = o;  o = align256(o + sizeof(float4) * 3 * k);
+        items = o; o = align256(o + sizeof(uint2) * (max_bwd_items(K, T) + 1));
+        total = o;
     }
 };
 

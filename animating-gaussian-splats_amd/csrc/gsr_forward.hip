@@ -181,7 +181,8 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
                                                    uint32_t *__restrict__ meta,
                                                    uint32_t *host_words,
                                                    uint32_t *__restrict__ tile_order,
-                                                   uint32_t *__restrict__ sort_lists) {
+                                                   uint32_t *__restrict__ sort_lists,
+                                                   uint32_t *__restrict__ seg_off) {
     __shared__ uint32_t s_red[16];
     __shared__ uint32_t s_hist[kOrderBuckets];
     __shared__ uint32_t s_cls[3];
@@ -208,6 +209,20 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
             }
             ex += cnt[i];
         }
+        // backward segment boundaries: exclusive prefix over tiles (index of each tile's first state)
+        uint32_t nbs = 0;
+#pragma unroll
+        for (int i = 0; i < kScanRegs; ++i) nbs += (i < c && t0 + i < T) ? seg_bounds(cnt[i]) : 0u;
+        uint32_t nbt;
+        uint32_t sex = block_excl_scan_u32(nbs, s_red, &nbt);
+#pragma unroll
+        for (int i = 0; i < kScanRegs; ++i) {
+            if (i < c && t0 + i < T) {
+                seg_off[t0 + i] = sex;
+                sex += seg_bounds(cnt[i]);
+            }
+        }
+        if (threadIdx.x == 0) seg_off[T] = nbt;
         uint32_t btot;
         const uint32_t bex = block_excl_scan_u32(bsum, s_red, &btot);  // contains the barrier s_cls needs
         if ((int)threadIdx.x < NB) block_off[threadIdx.x] = bex;
@@ -234,6 +249,16 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
         }
         carry += tot;
     }
+    uint32_t carry3 = 0;
+    for (int base = 0; base < T; base += blockDim.x) {
+        const int t = base + threadIdx.x;
+        const uint32_t nb = t < T ? seg_bounds(tile_count[t]) : 0;
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32(nb, s_red, &tot) + carry3;
+        if (t < T) seg_off[t] = ex;
+        carry3 += tot;
+    }
+    if (threadIdx.x == 0) seg_off[T] = carry3;
     uint32_t carry2 = 0;
     for (int base = 0; base < NB; base += blockDim.x) {
         const int b = base + threadIdx.x;
@@ -528,7 +553,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const uint4 *__restrict__ pairs,
     uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
-    float *__restrict__ final_T, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc) {
+    float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
+    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state) {
     __shared__ uint64_t s_key[kFwdSortCap];
     __shared__ union {
         uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
@@ -573,6 +599,13 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         __syncthreads();  // previous batch fully consumed; s_live up to date
         const uint32_t live = s_live;
         if (!live) break;
+        // segment boundary (kSeg entries): this quarter's blend state before entry `base`, the state a
+        // backward segment's reverse walk starts from; stored while the quarter is live, i.e. for
+        // every boundary below its pixels' last contributor (done pixels store their final state)
+        if (base > 0 && (base & (kSeg - 1)) == 0 && ((live >> wv) & 1u)) {
+            const size_t b = (size_t)seg_off[tile] + (uint32_t)base / kSeg - 1u;
+            seg_state[b * kTilePix + 64 * wv + lane] = make_float4(C0, C1, C2, Tt);
+        }
         // ---- stage the batch (block-wide) ----
         const int idx = base + se;
         bool hit = false;
@@ -614,7 +647,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     }
     if (inside) {
         const int pid = py * W + px;
-        final_T[pid] = Tt;
+        pix_end[pid] = make_float4(C0, C1, C2, Tt);
         n_contrib[pid] = last;
         out_color[pid] = C0 + Tt * bg[0];
         out_color[H * W + pid] = C1 + Tt * bg[1];
@@ -686,7 +719,7 @@ hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s
     const BinGrid bg(a.P);
     k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
                                   a.block_sums, a.block_off, a.meta, host_words, a.tile_order_f,
-                                  a.sort_lists);
+                                  a.sort_lists, a.seg_off);
     return hipGetLastError();
 }
 
@@ -712,8 +745,8 @@ hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_long, hipStream_t s) {
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
-                                   a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.final_T, a.n_contrib,
-                                   a.tile_maxc);
+                                   a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
+                                   a.tile_maxc, a.seg_off, a.seg_state);
     return hipGetLastError();
 }
 

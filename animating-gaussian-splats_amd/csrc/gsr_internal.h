@@ -19,11 +19,11 @@ struct FwdArgs {
     // geom
     float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff;
     // image
-    uint2 *ranges; float *final_T; uint32_t *n_contrib; uint32_t *tile_maxc;
-    uint32_t *tile_order_f; uint32_t *tile_order_b; uint32_t *sort_lists; uint32_t *tile_count;
+    uint2 *ranges; float4 *pix_end; uint32_t *n_contrib; uint32_t *tile_maxc;
+    uint32_t *tile_order_f; uint32_t *seg_off; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
     // binning
-    uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit;
+    uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
     int *radii; float *out_color; float *out_depth;
 };
@@ -37,9 +37,10 @@ struct BwdArgs {
     const int *radii;
     // saved state
     const float4 *rec; const uint2 *rect;
-    const uint32_t *goff; const uint2 *ranges; const float *final_T; const uint32_t *n_contrib;
-    const uint32_t *tile_maxc; uint32_t *tile_order_b;
-    const uint32_t *point_list; const uint32_t *slot_emit;
+    const uint32_t *goff; const uint2 *ranges; const float4 *pix_end; const uint32_t *n_contrib;
+    const uint32_t *tile_maxc; const uint32_t *seg_off; const uint32_t *meta;
+    const uint32_t *point_list; const uint32_t *slot_emit; const float4 *seg_state;
+    uint2 *items; uint32_t max_items;
     // scratch
     float4 *part;
     // upstream gradient
@@ -60,7 +61,7 @@ hipError_t launch_zero(float *p, size_t n, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 
-hipError_t launch_tile_order_bwd(const BwdArgs &a, hipStream_t s);
+hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 

@@ -85,9 +85,11 @@ def load_library():
     L.gsr_grad_fence.argtypes = [ctypes.POINTER(vp), i, vp]
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
-    for n in ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_scratch_bytes"):
+    for n in ("gsr_geom_bytes", "gsr_binning_bytes"):
         getattr(L, n).restype = ctypes.c_size_t
         getattr(L, n).argtypes = [i]
+    L.gsr_scratch_bytes.restype = ctypes.c_size_t
+    L.gsr_scratch_bytes.argtypes = [i, i, i]
     L.gsr_image_bytes.restype = ctypes.c_size_t
     L.gsr_image_bytes.argtypes = [i, i, i]
     L.gsr_last_error.restype = ctypes.c_char_p
@@ -114,7 +116,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 10  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 11  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -363,8 +365,8 @@ def profile_read(phase=None):
 def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
     """Typed views of the arrays inside the forward buffers (for parity tests / debugging)."""
     L = load_library()
-    offs = (ctypes.c_size_t * 12)()
-    L.gsr_buffer_offsets(int(P), int(W), int(H), int(num_rendered), offs, 12)
+    offs = (ctypes.c_size_t * 14)()
+    L.gsr_buffer_offsets(int(P), int(W), int(H), int(num_rendered), offs, 14)
     o = list(offs)
     T = ((W + 15) // 16) * ((H + 15) // 16)
     K = int(num_rendered)
@@ -386,7 +388,9 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
         "tiles_touched": view(geomBuffer, o[3], P, i32, (P,)),
         "goff": view(geomBuffer, o[4], P + 1, i32, (P + 1,)),
         "ranges": view(imgBuffer, o[5], 2 * T, i32, (T, 2)),
-        "final_T": view(imgBuffer, o[6], W * H, f32, (H, W)),
+        "pix_end": view(imgBuffer, o[6], 4 * W * H, f32, (H, W, 4)),
+        "final_T": view(imgBuffer, o[6], 4 * W * H, f32, (H, W, 4))[..., 3],
+        "seg_off": view(imgBuffer, o[12], T + 1, i32, (T + 1,)),
         "n_contrib": view(imgBuffer, o[7], W * H, i32, (H, W)),
         "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
         # per-pair records (index, depth bits, emission, 0) in tile-bucket order; keys = .x | .y << 32

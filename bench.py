@@ -42,7 +42,7 @@ PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_hbm_pmc.json")
 # SQ counters of the same command (tools/profile_round.sh sq passes): VALU activity per launch
 SQ_SUMMARY = os.path.join(REPO, "profiles", "r01_sq_pmc.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
-PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "tile_order_bwd",
+PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "bwd_items",
           "render_bwd", "gauss_bwd"]
 
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 10
+#define GSR_ABI_VERSION 11
 
 enum gsr_status {
     GSR_OK = 0,
@@ -162,11 +162,15 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 size_t gsr_geom_bytes(int P);
 size_t gsr_image_bytes(int width, int height, int P);
 size_t gsr_binning_bytes(int num_rendered);
-size_t gsr_scratch_bytes(int num_rendered);
+size_t gsr_scratch_bytes(int num_rendered, int width, int height);
 
 /* Introspection for parity tests: byte offsets of the arrays inside the three forward buffers, in
  * this order: geom {depth, rec (64-byte render records), rect, tiles, goff}, image {ranges,
- * final_T, n_contrib, tile_maxc}, binning {pairs (16-byte records: index, depth bits, emission, 0), point_list, slot_emit}.  Returns the count written (12). */
+ * pix_end (per pixel float4: accumulated colour without background, final transmittance),
+ * n_contrib, tile_maxc}, binning {pairs (16-byte records: index, depth bits, emission, 0),
+ * point_list, slot_emit}, image {seg_off}, binning {seg_state (the blend state at every interior
+ * 128-entry boundary of every tile list: 256 float4 (C0, C1, C2, T) per boundary)}.  Returns the
+ * count written (14). */
 int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *out, int max_out);
 
 const char *gsr_last_error(void);
@@ -282,7 +286,7 @@ int gsr_views_pack(int frames, int H, int W, const uint8_t *rgb, const uint8_t *
 
 /* Per-phase device timing with HIP events recorded on the call's stream (off by default).
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
- * "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam", "views_pack".  gsr_profile_read synchronises on the recorded events. */
+ * "bwd_items", "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam", "views_pack".  gsr_profile_read synchronises on the recorded events. */
 int gsr_profile_enable(int on);
 /* Restrict event recording to a comma-separated list of phases (NULL or "" = every phase), so a
  * timed region can carry the events of one kernel only.  Host-side timers are unaffected. */

@@ -38,13 +38,13 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     L = _C.load_library()
-    assert L.gsr_abi_version() == _C.ABI_VERSION == 10
+    assert L.gsr_abi_version() == _C.ABI_VERSION == 11
     for P in (0, 1, 1000, 1_000_000):
         assert L.gsr_geom_bytes(P) % 256 == 0 and L.gsr_geom_bytes(P) >= 64 * P
     assert L.gsr_image_bytes(1920, 1080, 10) >= 1920 * 1080 * 8
-    assert L.gsr_binning_bytes(100) >= 100 * 16 and L.gsr_scratch_bytes(100) >= 100 * 36
-    offs = (ctypes.c_size_t * 12)()
-    assert L.gsr_buffer_offsets(100, 64, 48, 500, offs, 12) == 12
+    assert L.gsr_binning_bytes(100) >= 100 * 16 and L.gsr_scratch_bytes(100, 64, 48) >= 100 * 36
+    offs = (ctypes.c_size_t * 14)()
+    assert L.gsr_buffer_offsets(100, 64, 48, 500, offs, 14) == 14
     assert all(o % 256 == 0 for o in offs)
 
 

@@ -85,7 +85,7 @@ def main():
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
     fbuf = torch.zeros(4 * 4 * T, dtype=torch.int64, device=dev)
-    bbuf = torch.zeros(4 * 4 * T, dtype=torch.int64, device=dev)
+    bbuf = torch.zeros(4 * 16 * T, dtype=torch.int64, device=dev)  # (tile, segment) items
     L.gsr_debug_trace_fwd.argtypes = [ctypes.c_void_p]
     L.gsr_debug_trace_bwd.argtypes = [ctypes.c_void_p]
     L.gsr_debug_trace_emit.argtypes = [ctypes.c_void_p]
@@ -102,10 +102,10 @@ def main():
         img.backward(dl)
         torch.cuda.synchronize()
         L.gsr_debug_trace_fwd(None); L.gsr_debug_trace_bwd(None); L.gsr_debug_trace_emit(None)
-        np.save(os.path.join(REPO, "gpurun_out", f"trace_bwd_cam{ci}.npy"), bbuf.cpu().numpy()[: 4 * T])
+        np.save(os.path.join(REPO, "gpurun_out", f"trace_bwd_cam{ci}.npy"), bbuf.cpu().numpy())
         report[ci] = {"emit": analyse_emit(ebuf.cpu().numpy(), f"cam{ci} emit"),
                       "fwd": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd"),
-                      "bwd": analyse(bbuf.cpu().numpy(), T, f"cam{ci} bwd")}
+                      "bwd": analyse(bbuf.cpu().numpy(), 16 * T, f"cam{ci} bwd")}
     out = os.path.join(REPO, "gpurun_out")
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "render_trace.json"), "w") as f:
