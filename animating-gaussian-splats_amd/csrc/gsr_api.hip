@@ -314,12 +314,18 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     }
     if (K > 0x7FFFFFFFu) return fail(GSR_ERR_UNSUPPORTED, "num_rendered overflow");
     *out_num_rendered = (int)K;
-    char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)K).total);
+    // tiles to sort outside the render: [1] up to kSortCap pairs, [2] longer (merge sort), [3] the
+    // longest list (merge passes); the latter need a temporary copy of the pair records
+    const uint32_t n_mid = __atomic_load_n(hw.h + 1, __ATOMIC_ACQUIRE);
+    const uint32_t n_vlong = __atomic_load_n(hw.h + 2, __ATOMIC_ACQUIRE);
+    const uint32_t max_n = __atomic_load_n(hw.h + 3, __ATOMIC_ACQUIRE);
+    const size_t bin_bytes = BinningLayout((int)K).total;
+    const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
+    char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, bin_bytes + tmp_bytes);
     if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
     carve_binning(a, bin, (int)K);
     { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, (int)K, s)); }
-    const uint32_t n_long = __atomic_load_n(hw.h + 1, __ATOMIC_ACQUIRE);
-    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_long, s)); }
+    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)(bin + bin_bytes), s)); }
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     return GSR_OK;
 }

@@ -21,7 +21,8 @@ constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (
 __host__ __device__ inline uint64_t pair_key(uint4 r) { return ((uint64_t)r.y << 32) | r.x; }
 constexpr int kFwdSortCap = 1024;  // lists up to this length are depth-sorted inside k_render_fwd
 // host-mapped words published by k_bin_scan: [0] = K (written last, release), [1] = number of
-// tiles longer than kFwdSortCap (sorted by k_tile_sort before the render), [2..3] unused
+// tiles with kFwdSortCap < n <= kSortCap pairs (k_tile_sort), [2] = number of longer tiles (chunk
+// sort + merge passes), [3] = the longest list
 constexpr int kHostWords = 4;
 
 __host__ __device__ inline int div_up(int a, int b) { return (a + b - 1) / b; }

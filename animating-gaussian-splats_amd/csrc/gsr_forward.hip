@@ -205,7 +205,12 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
             if (i < c && t < T) {
                 ranges[t] = cnt[i] ? make_uint2(ex, ex + cnt[i]) : make_uint2(0, 0);  // empty: {0,0} like the reference
                 tile_cursor[t] = ex;
-                if (cnt[i] > (uint32_t)kFwdSortCap) sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
+                if (cnt[i] > (uint32_t)kSortCap) {  // long: merge-sorted; listed from the end
+                    sort_lists[T - 1 - atomicAdd(&s_cls[1], 1u)] = (uint32_t)t;
+                    atomicMax(&s_cls[2], cnt[i]);
+                } else if (cnt[i] > (uint32_t)kFwdSortCap) {
+                    sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
+                }
             }
             ex += cnt[i];
         }
@@ -273,7 +278,12 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
     for (int t = threadIdx.x; t < T; t += blockDim.x) {
         const uint32_t n = tile_count[t];
         if (n == 0) continue;
-        if (n > (uint32_t)kFwdSortCap) sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
+        if (n > (uint32_t)kSortCap) {
+            sort_lists[T - 1 - atomicAdd(&s_cls[1], 1u)] = (uint32_t)t;
+            atomicMax(&s_cls[2], n);
+        } else if (n > (uint32_t)kFwdSortCap) {
+            sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -482,9 +492,8 @@ __device__ inline void block_sort_tile(int n, uint32_t start, const uint4 *__res
     __syncthreads();
 }
 
-// Tiles longer than kFwdSortCap (one 512-thread block each, launched only for those tiles): up to
-// kSortCap pairs with the register + LDS hybrid of block_sort_tile over 8 waves (4 or 8 keys per
-// lane); beyond that an in-place bitonic network in global memory.
+// Tiles longer than kFwdSortCap and at most kSortCap pairs (one 512-thread block each, launched only
+// for those tiles): the register + LDS hybrid of block_sort_tile over 8 waves (4 or 8 keys per lane).
 __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
                                                     const uint2 *__restrict__ ranges,
                                                     uint4 *__restrict__ pairs,
@@ -495,47 +504,110 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
     const int tile = (int)tiles[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
-    const int tid = threadIdx.x, nt = blockDim.x;
-    if (n <= kSortCap) {
-        static_assert(kSortCap == 8 * 64 * 8, "k_tile_sort: 8 waves x 64 lanes x 8 keys");
-        if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, pairs, s_keys, s_vals);
-        else block_sort_tile<8, 8>(n, rg.x, pairs, s_keys, s_vals);
-        for (int i = tid; i < n; i += nt) {
-            point_list[rg.x + i] = (uint32_t)s_keys[i];
-            slot_emit[rg.x + i] = s_vals[i];
-        }
-    } else {
-        // long tile: in-place bitonic network in global memory with virtual +inf padding
-        // ("flip" form: every comparator puts the minimum at the lower index).
-        uint4 *a = pairs + rg.x;
-        int np = 1;
-        while (np < n) np <<= 1;
-        for (int k = 2; k <= np; k <<= 1) {
-            const int h = k >> 1;
-            for (int i = tid; i < (np >> 1); i += nt) {
-                const int lo = ((i & ~(h - 1)) << 1) | (i & (h - 1)), hi = lo ^ (k - 1);
-                if (hi < n) {
-                    const uint4 x = a[lo], y = a[hi];
-                    if (pair_key(x) > pair_key(y)) { a[lo] = y; a[hi] = x; }
-                }
-            }
-            __syncthreads();
-            for (int j = k >> 2; j > 0; j >>= 1) {
-                for (int i = tid; i < (np >> 1); i += nt) {
-                    const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1)), hi = lo + j;
-                    if (hi < n) {
-                        const uint4 x = a[lo], y = a[hi];
-                        if (pair_key(x) > pair_key(y)) { a[lo] = y; a[hi] = x; }
-                    }
-                }
-                __syncthreads();
-            }
-        }
-        for (int i = tid; i < n; i += nt) {
-            const uint4 q = a[i];
-            point_list[rg.x + i] = q.x;
-            slot_emit[rg.x + i] = q.z;
-        }
+    static_assert(kSortCap == 8 * 64 * 8, "k_tile_sort: 8 waves x 64 lanes x 8 keys");
+    if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, pairs, s_keys, s_vals);
+    else block_sort_tile<8, 8>(n, rg.x, pairs, s_keys, s_vals);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        point_list[rg.x + i] = (uint32_t)s_keys[i];
+        slot_emit[rg.x + i] = s_vals[i];
+    }
+}
+
+// ---- lists longer than kSortCap: multi-block merge sort -------------------------------------
+// (a densified scene's dense tiles: tens of thousands of pairs in one tile).  The tile's range is
+// cut into kSortCap chunks, each sorted in LDS by its own block (k_chunk_sort, block_sort_tile,
+// written back in place as 16-byte records), then log2(n / kSortCap) merge passes double the sorted
+// run length (k_merge_pass): every block produces kSortCap outputs of one pair of runs, finding its
+// share of each run by a merge-path search (64-ary, one wave per end of the window), staging that
+// window in LDS and merging 8 outputs per thread.  Passes ping-pong between the pair records and a
+// temporary copy; the last one writes the point list and the slot -> emission map.  Keys
+// (depth bits << 32 | index) are unique inside a tile, so the order is exactly the stable (tile,
+// depth) order of the reference's radix sort.  Grid: (max chunks of a long tile, long tiles).
+__device__ inline uint4 key_record(uint64_t k, uint32_t emit) {
+    return make_uint4((uint32_t)k, (uint32_t)(k >> 32), emit, 0u);
+}
+
+__global__ __launch_bounds__(512) void k_chunk_sort(int T, const uint32_t *__restrict__ lists,
+                                                     const uint2 *__restrict__ ranges, uint4 *__restrict__ pairs) {
+    __shared__ uint64_t s_keys[kSortCap];
+    __shared__ uint32_t s_vals[kSortCap];
+    const int tile = (int)lists[T - 1 - (int)blockIdx.y];  // long tiles are listed from the end
+    const uint2 rg = ranges[tile];
+    const int n = (int)(rg.y - rg.x);
+    const int c0 = (int)blockIdx.x * kSortCap;
+    if (c0 >= n) return;
+    const int m = min(kSortCap, n - c0);
+    block_sort_tile<8, 8>(m, rg.x + c0, pairs, s_keys, s_vals);
+    for (int i = threadIdx.x; i < m; i += blockDim.x) pairs[rg.x + c0 + i] = key_record(s_keys[i], s_vals[i]);
+}
+
+// Merge-path split of diagonal d between sorted runs a (length la) and b (length lb): the number of
+// a's elements among the first d outputs.  One wave, 64 probes per round.
+__device__ inline uint32_t merge_split(const uint4 *__restrict__ a, uint32_t la, const uint4 *__restrict__ b,
+                                       uint32_t lb, uint32_t d) {
+    const int lane = threadIdx.x & 63;
+    uint32_t lo = d > lb ? d - lb : 0u, hi = min(d, la);  // answer in [lo, hi]
+    while (lo < hi) {
+        const uint32_t span = hi - lo, step = (span + 63) / 64;
+        const uint32_t x = lo + (uint32_t)lane * step;
+        // P(x): a[x] precedes b[d - 1 - x] (true for a prefix of x, false after)
+        const bool p = x < hi && pair_key(a[x]) < pair_key(b[d - 1 - x]);
+        const uint32_t c = (uint32_t)__popcll(__ballot(p));
+        const uint32_t nlo = c ? lo + (c - 1) * step + 1 : lo;
+        const uint32_t nhi = min(hi, lo + c * step);
+        lo = nlo;
+        hi = max(nlo, nhi);
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(512) void k_merge_pass(int T, const uint32_t *__restrict__ lists,
+                                                     const uint2 *__restrict__ ranges, uint32_t L,
+                                                     const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                     int final_pass, uint32_t *__restrict__ point_list,
+                                                     uint32_t *__restrict__ slot_emit) {
+    __shared__ uint64_t s_ka[kSortCap], s_kb[kSortCap];
+    __shared__ uint32_t s_va[kSortCap], s_vb[kSortCap];
+    __shared__ uint32_t s_split[2];
+    const int tile = (int)lists[T - 1 - (int)blockIdx.y];
+    const uint2 rg = ranges[tile];
+    const uint32_t n = rg.y - rg.x;
+    const uint32_t o0 = blockIdx.x * (uint32_t)kSortCap;
+    if (o0 >= n) return;
+    const uint32_t pb = o0 / (2 * L) * (2 * L);                    // this pair of runs starts here
+    const uint32_t la = min(L, n - pb), lb = n - pb > L ? min(L, n - pb - L) : 0u;
+    const uint4 *a = src + rg.x + pb, *b = a + la;
+    const uint32_t d0 = o0 - pb, d1 = min(d0 + (uint32_t)kSortCap, la + lb);
+    const int wv = threadIdx.x >> 6;
+    if (wv < 2) {
+        const uint32_t sp = merge_split(a, la, b, lb, wv == 0 ? d0 : d1);
+        if ((threadIdx.x & 63) == 0) s_split[wv] = sp;
+    }
+    __syncthreads();
+    const uint32_t i0 = s_split[0], i1 = s_split[1], j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t na = i1 - i0, nb = j1 - j0;
+    for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) { const uint4 q = a[i0 + i]; s_ka[i] = pair_key(q); s_va[i] = q.z; }
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) { const uint4 q = b[j0 + i]; s_kb[i] = pair_key(q); s_vb[i] = q.z; }
+    __syncthreads();
+    // 8 consecutive outputs per thread: its diagonal's split in LDS, then a sequential merge
+    constexpr uint32_t kPer = kSortCap / 512;
+    const uint32_t dl = threadIdx.x * kPer;
+    if (dl >= na + nb) return;
+    uint32_t lo = dl > nb ? dl - nb : 0u, hi = min(dl, na);
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_ka[mid] < s_kb[dl - 1 - mid]) lo = mid + 1; else hi = mid;
+    }
+    uint32_t ia = lo, ib = dl - lo;
+    const uint32_t e = min(dl + kPer, na + nb);
+    for (uint32_t o = dl; o < e; ++o) {
+        const bool take_a = ib >= nb || (ia < na && s_ka[ia] < s_kb[ib]);
+        const uint64_t k = take_a ? s_ka[ia] : s_kb[ib];
+        const uint32_t v = take_a ? s_va[ia] : s_vb[ib];
+        ia += take_a; ib += !take_a;
+        const size_t slot = (size_t)rg.x + pb + d0 + o;
+        if (final_pass) { point_list[slot] = (uint32_t)k; slot_emit[slot] = v; }
+        else dst[slot] = key_record(k, v);
     }
 }
 
@@ -734,11 +806,26 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_long, hipStream_t s) {
-    // lists of up to kFwdSortCap pairs are sorted inside k_render_fwd; only longer ones here
-    if (n_long == 0) return hipSuccess;
-    k_tile_sort<<<n_long, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs,
-                                        a.point_list, a.slot_emit);
+hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, uint32_t max_n, uint4 *tmp,
+                            hipStream_t s) {
+    // lists of up to kFwdSortCap pairs are sorted inside k_render_fwd; up to kSortCap by one block
+    // per tile; longer ones by chunk sorts + merge passes
+    const int T = a.gx * a.gy;
+    if (n_mid) k_tile_sort<<<n_mid, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs, a.point_list, a.slot_emit);
+    if (n_vlong) {
+        const dim3 grid((unsigned)div_up((int)max_n, kSortCap), n_vlong);
+        k_chunk_sort<<<grid, 512, 0, s>>>(T, a.sort_lists, a.ranges, a.pairs);
+        const uint4 *src = a.pairs;
+        uint4 *dst = tmp;
+        for (uint32_t L = kSortCap; L < max_n; L *= 2) {
+            const int final_pass = 2 * (size_t)L >= max_n;
+            k_merge_pass<<<grid, 512, 0, s>>>(T, a.sort_lists, a.ranges, L, src, dst, final_pass, a.point_list,
+                                              a.slot_emit);
+            const uint4 *t = dst;
+            dst = const_cast<uint4 *>(src);
+            src = t;
+        }
+    }
     return hipGetLastError();
 }
 

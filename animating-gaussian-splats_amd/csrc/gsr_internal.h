@@ -55,7 +55,8 @@ hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);
 hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s);
 hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s);
 hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s);
-hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_long, hipStream_t s);
+hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, uint32_t max_n, uint4 *tmp,
+                            hipStream_t s);
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s);
 hipError_t launch_zero(float *p, size_t n, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,

@@ -212,10 +212,11 @@ def test_depth_ties_follow_index_order(cuda):
     check_forward(fw, st)
 
 
-@pytest.mark.parametrize("P", [800, 2_500, 12_000])
+@pytest.mark.parametrize("P", [800, 2_500, 12_000, 50_000, 200_000])
 def test_long_tile_lists(P, cuda):
     """Clustered Gaussians: tile lists of ~P entries exercise every sort path (registers up to 512
-    and 1024 pairs, LDS bitonic up to 4096, in-place global bitonic beyond)."""
+    and 1024 pairs inside the render, one LDS block up to 4096, chunk sorts + merge passes beyond:
+    50k pairs = 13 chunks, 4 passes; 200k = 49 chunks, 6 passes)."""
     g = torch.Generator().manual_seed(4)
     m = torch.zeros(P, 3)
     m[:, 0] = torch.rand(P, generator=g) * 0.02 - 0.01
