@@ -51,11 +51,12 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 #pragma unroll
             for (int i = 0; i < kScanRegs; ++i) {
                 const uint32_t t = (uint32_t)(t0 + i * (int)blockDim.x + (int)threadIdx.x);
-                const uint32_t J = bwd_item_count(nn[i], mq[i]);
-                for (uint32_t j = 0; j < J; ++j) {
-                    const uint32_t b = bucket(bwd_item_cost(j, mq[i]) + kItemStartCost);
+                const uint32_t J = bwd_item_count(nn[i], mq[i]), Z = bwd_zero_items(nn[i], mq[i]);
+                for (uint32_t j = 0; j < J + Z; ++j) {
+                    const uint32_t cost = j < J ? bwd_item_cost(j, mq[i]) + kItemStartCost : kItemStartCost;
+                    const uint32_t b = bucket(cost);
                     if (pass == 0) atomicAdd(&s_hist[b], 1u);
-                    else items[1 + atomicAdd(&s_hist[b], 1u)] = make_uint2(t, j);
+                    else items[1 + atomicAdd(&s_hist[b], 1u)] = make_uint2(t, j < J ? j : kZeroItem | (j - J));
                 }
             }
         }
@@ -119,10 +120,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
     const float tx1 = tx0 + (kTileW - 1);
     const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
     const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
+    if (seg & kZeroItem) {  // zero records for one kZeroChunk of the slots past maxc (see bwd_zero_items)
+        const int z0 = maxc + (int)kZeroChunk * (int)((seg & ~kZeroItem) + 1);
+        for (int p = z0 + lane; p < min(n, z0 + (int)kZeroChunk); p += 64) {
+            float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
+            dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dst[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
     const int s0 = (int)seg * kSeg, s1f = s0 + kSeg;
     const int s1 = min(s1f, maxc);
-    if (s1f >= maxc) {  // the tile's last item: slots nobody reached get zero records
-        for (int p = maxc + lane; p < n; p += 64) {
+    if (s1f >= maxc) {  // the tile's last segment item: the first kZeroChunk slots nobody reached
+        for (int p = maxc + lane; p < min(n, maxc + (int)kZeroChunk); p += 64) {
             float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
             dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
             dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -72,6 +72,9 @@ struct BinGrid {
 // (front colour, transmittance) before entry kSeg, 2 kSeg, ... of its tile: the state a segment's
 // reverse walk starts from.  A power of two >= the forward's 64-entry batch (k_render_fwd tests
 // boundaries with a mask).  256: measured against 128 / 512 / 1024 (tools/ab_variants.sh).
+#ifndef GSR_FWD_PREFETCH
+#define GSR_FWD_PREFETCH 1  // k_render_fwd loads each batch's records during the previous blend
+#endif
 #ifndef GSR_KSEG
 #define GSR_KSEG 256
 #endif
@@ -92,10 +95,20 @@ __host__ __device__ inline uint32_t bwd_item_cost(uint32_t j, uint4 mq) {
     const uint32_t c = mq.z > s0 ? min(mq.z, s1) - s0 : 0u, d = mq.w > s0 ? min(mq.w, s1) - s0 : 0u;
     return a + b + c + d;
 }
+// Zero-record items: a tile's list entries past every pixel's last contributor (maxc .. n) get zero
+// gradient records (k_gauss_bwd sums every emission slot); the tile's last segment item writes the
+// first kZeroChunk of them, every further kZeroChunk is an item of its own (seg = kZeroItem | chunk),
+// so a long list whose pixels saturated early does not leave one wave storing all of them.
+constexpr uint32_t kZeroChunk = 1024;
+constexpr uint32_t kZeroItem = 0x80000000u;
+__host__ __device__ inline uint32_t bwd_zero_items(uint32_t n, uint4 mq) {
+    const uint32_t maxc = min(max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
+    return n - maxc > kZeroChunk ? (n - maxc - 1) / kZeroChunk : 0u;
+}
 // the upper bound of the item count the backward launch covers
 __host__ __device__ inline size_t max_bwd_items(int K, int T) {
     const size_t k = (size_t)(K > 0 ? K : 0);
-    return k / kSeg + (k < (size_t)T ? k : (size_t)T) + 1;
+    return k / kSeg + k / kZeroChunk + (k < (size_t)T ? k : (size_t)T) + 1;
 }
 
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.

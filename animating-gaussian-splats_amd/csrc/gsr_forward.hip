@@ -667,6 +667,25 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     if (__ballot(!done) && lane == 0) atomicOr(&s_live, 1u << wv);
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
     uint32_t last = 0;
+#if GSR_FWD_PREFETCH
+    // entry se of the NEXT batch: its render record halves (x, y, conic; colour) in registers, loaded
+    // one batch ahead so the gathers' latency hides behind the current batch's blend
+    float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pr = pa;
+    bool pv = false;
+#define GSR_FWD_FETCH(bse)                                                                         \
+    do {                                                                                           \
+        const int idx_ = (bse) + se;                                                               \
+        pv = idx_ < n;                                                                             \
+        if (pv) {                                                                                  \
+            const uint32_t g_ = sorted_here ? (uint32_t)s_key[idx_] : point_list[rg.x + idx_];      \
+            const float4 *r_ = rec + (size_t)kRecF4 * g_;                                          \
+            pa = r_[0];                                                                            \
+            pb = r_[1];                                                                            \
+            pr = r_[sq < 3 ? sq : 2];                                                              \
+        }                                                                                          \
+    } while (0)
+    GSR_FWD_FETCH(0);
+#endif
     for (int base = 0; base < n; base += 64) {
         __syncthreads();  // previous batch fully consumed; s_live up to date
         const uint32_t live = s_live;
@@ -679,8 +698,19 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             seg_state[b * kTilePix + 64 * wv + lane] = make_float4(C0, C1, C2, Tt);
         }
         // ---- stage the batch (block-wide) ----
-        const int idx = base + se;
         bool hit = false;
+#if GSR_FWD_PREFETCH
+        {   // this batch's records were loaded during the previous batch's blend
+            const float4 a = pa, b = pb;
+            if (pv) {
+                if (sq < 3) s_u.st.rec[sq][se] = pr;
+                hit = ((live >> sq) & 1u) &&
+                      !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kTileW - 1), qy0 + 3);
+            }
+            GSR_FWD_FETCH(base + 64);
+        }
+#else
+        const int idx = base + se;
         if (idx < n) {
             const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1];
@@ -688,6 +718,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             hit = ((live >> sq) & 1u) &&
                   !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kTileW - 1), qy0 + 3);
         }
+#endif
         // combine the 4 quarter bits of entry se (lanes 4e..4e+3 of this wave) with DPP
         uint32_t bits = hit ? (1u << sq) : 0u;
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xF, 0xF, false);  // xor 1

@@ -113,6 +113,25 @@ def synthetic_cloud(P: int, s0: float, sh_degree: int = -1, seed: int = 0, devic
     return {k: v.float().contiguous().to(device) for k, v in out.items()}
 
 
+def clustered_cloud(P: int, s0: float, sh_degree: int = -1, seed: int = 0, clusters: int = 16,
+                    spread: float = 0.03, device="cuda") -> dict:
+    """A densified-scene stand-in: the synthetic_cloud parameters with half of the means moved into
+    `clusters` tight Gaussian blobs (std `spread`, centres uniform in the same box), so the tiles over
+    a blob hold tens of thousands of Gaussian-tile pairs (the long-list sort and the backward's
+    segment items at work) while the rest of the image stays like the uniform cloud."""
+    out = synthetic_cloud(P, s0, sh_degree=sh_degree, seed=seed, device="cpu")
+    g = torch.Generator().manual_seed(seed + 1000)
+    lo = torch.tensor([-2.2, -1.25, -1.0])
+    hi = torch.tensor([2.2, 1.25, 1.0])
+    centres = lo + (hi - lo) * torch.rand(clusters, 3, generator=g)
+    m = P // 2
+    which = torch.randint(0, clusters, (m,), generator=g)
+    means = out["means"].clone()
+    means[:m] = centres[which] + spread * torch.randn(m, 3, generator=g)
+    out["means"] = means.contiguous()
+    return {k: v.to(device) for k, v in out.items()}
+
+
 def upstream_grad(H: int, W: int, seed: int = 1, device="cuda") -> torch.Tensor:
     g = torch.Generator().manual_seed(seed)
     return torch.randn(3, H, W, generator=g).to(device)

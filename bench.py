@@ -457,12 +457,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="C3", choices=["C3", "C4", "C5"],
+    ap.add_argument("--config", default="C3", choices=["C3", "C3M", "C4", "C5"],
                     help="C3 (default): 1M Gaussians SH3 at 1080p, --views-per-rank rig views per GPU per "
                          "step (weak scaling); C4: 1M Gaussians, the 27-camera rig sharded round-robin over "
                          "the ranks per step + one RCCL SUM all-reduce (strong scaling); C5: 2M Gaussians x "
                          "150-frame sequence, frames sharded in blocks, one per-frame optimisation iteration "
-                         "(5 views, fused L1+SSIM, fused Adam) per GPU per step, no collective (weak scaling)")
+                         "(5 views, fused L1+SSIM, fused Adam) per GPU per step, no collective (weak scaling); "
+                         "C3M: C3 with half of the means in 16 tight clusters (a densified scene: tiles of "
+                         "tens of thousands of pairs)")
     ap.add_argument("--views-per-rank", type=int, default=5,
                     help="C3 / C5: views rendered per GPU per step (train.py:753 optimises on the summed "
                          "losses of 5 views per step)")
@@ -524,10 +526,13 @@ def main():
     if args.config == "C5":
         cfg = S.SceneConfig("C5", 2_000_000, 1920, 1080, 1600.0, 0.005, views=S.RIG27)
     else:
-        base = S.CONFIGS[args.config]
-        cfg = S.SceneConfig(base.name, base.P, base.width, base.height, base.focal, base.s0,
+        base = S.CONFIGS["C3" if args.config == "C3M" else args.config]
+        cfg = S.SceneConfig(args.config, base.P, base.width, base.height, base.focal, base.s0,
                             sh_degree=base.sh_degree, views=S.RIG27)
-    params_cpu = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0, device="cpu")
+    if args.config == "C3M":
+        params_cpu = S.clustered_cloud(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0, device="cpu")
+    else:
+        params_cpu = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0, device="cpu")
     params = {k: torch.nn.Parameter(v.to(dev)) for k, v in params_cpu.items()}
     cams = S.scene_cameras(cfg, device=dev)
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
@@ -674,7 +679,7 @@ def main():
     first = args.warmup + args.probe_steps
     used = c5.used_views(first, args.steps) if c5 else \
         sorted({ci for it in range(first, first + args.steps) for ci in views_of(it)})
-    Ks = []
+    Ks, max_tile = [], 0
     with torch.no_grad():
         a = c5.frame_inputs(c5.frames[0]) if c5 else S.activated_inputs(params, cfg.sh_degree)
         if cfg.sh_degree >= 0:
@@ -683,11 +688,14 @@ def main():
         colors = a.get("colors_precomp")
         for ci in used:
             c = cams[ci]
-            Ks.append(_C.rasterize_gaussians(c.bg, a["means3D"], colors if colors is not None else e,
-                                             a["opacities"], a["scales"], a["rotations"], 1.0, e,
-                                             c.viewmatrix, c.projmatrix, c.tanfovx, c.tanfovy,
-                                             cfg.height, cfg.width, a.get("shs", e), c.sh_degree,
-                                             c.campos, False)[0])
+            r = _C.rasterize_gaussians(c.bg, a["means3D"], colors if colors is not None else e,
+                                       a["opacities"], a["scales"], a["rotations"], 1.0, e,
+                                       c.viewmatrix, c.projmatrix, c.tanfovx, c.tanfovy,
+                                       cfg.height, cfg.width, a.get("shs", e), c.sh_degree,
+                                       c.campos, False)
+            Ks.append(r[0])
+            rg = _C.decode_buffers(a["means3D"].shape[0], cfg.width, cfg.height, r[0], r[3], r[4], r[5])["ranges"]
+            max_tile = max(max_tile, int((rg[:, 1] - rg[:, 0]).max()))
     K = float(np.mean(Ks))
     N = cfg.width * cfg.height
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
@@ -731,6 +739,8 @@ def main():
         workload = {
             "C3": f"C3: {cfg.P} Gaussians, SH{cfg.sh_degree}, {cfg.width}x{cfg.height}, 27-camera rig, "
                   f"{V} view(s)/GPU/step, fwd+bwd" + (", RCCL SUM all-reduce of the gradients" if world > 1 else ""),
+            "C3M": f"C3M: C3 with half of the {cfg.P} means in 16 tight clusters (densified-scene stand-in), "
+                   f"SH{cfg.sh_degree}, {cfg.width}x{cfg.height}, {V} view(s)/GPU/step, fwd+bwd",
             "C4": f"C4: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, the 27-camera rig per step sharded "
                   f"round-robin over {world} GPU(s), fwd+bwd" + (", one RCCL SUM all-reduce" if world > 1 else ""),
             "C5": f"C5: {cfg.P} Gaussians x 150 frames, RGB, {cfg.width}x{cfg.height}, frames sharded in blocks "
@@ -748,7 +758,7 @@ def main():
                        "views_per_gpu": [len(splat_dp.shard_views(list(range(views_per_step)), r, world))
                                          for r in range(world)],
                        "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
-                       "mean_num_rendered": int(K), "parallelism": f"camera-dp{world}" if args.config != "C5"
+                       "mean_num_rendered": int(K), "max_tile_pairs": max_tile, "parallelism": f"camera-dp{world}" if args.config != "C5"
                        else f"frame-dp{world}", "streams_per_gpu": len(streams),
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),

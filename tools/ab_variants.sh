@@ -6,7 +6,7 @@ mkdir -p gpurun_out/ab
 for rep in 1 2; do
   for v in "$@"; do
     for st in 3 1; do
-      GSR_LIB=$(pwd)/tools/ab/libgsr_$v.so timeout -k 10 200 python -u bench.py --streams $st --steps 40 \
+      GSR_LIB=$(pwd)/tools/ab/libgsr_$v.so timeout -k 10 200 python -u bench.py --streams $st --steps 40 ${BENCH_ARGS:-} \
         --call-site-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0 --no-cpu-baseline \
         > gpurun_out/ab/$v.$st.$rep.json 2> gpurun_out/ab/$v.$st.$rep.err || { echo "$v failed"; tail -5 gpurun_out/ab/$v.$st.$rep.err; exit 1; }
       python -c "

@@ -71,11 +71,11 @@ def main():
     from diff_gaussian_rasterization import GaussianRasterizer, _C
     L = _C.load_library()
     dev = torch.device("cuda", 0)
-    base = S.CONFIGS[args.config]
+    base = S.CONFIGS["C3" if args.config == "C3M" else args.config]
     cfg = S.SceneConfig(base.name, base.P, base.width, base.height, base.focal, base.s0,
                         sh_degree=base.sh_degree, views=S.RIG27)
-    params = {k: v.to(dev) for k, v in S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0,
-                                                          device="cpu").items()}
+    gen = S.clustered_cloud if args.config == "C3M" else S.synthetic_cloud
+    params = {k: v.to(dev) for k, v in gen(cfg.P, cfg.s0, sh_degree=cfg.sh_degree, seed=0, device="cpu").items()}
     with torch.no_grad():
         act = S.activated_inputs(params, cfg.sh_degree)
     if cfg.sh_degree >= 0:
@@ -103,6 +103,7 @@ def main():
         torch.cuda.synchronize()
         L.gsr_debug_trace_fwd(None); L.gsr_debug_trace_bwd(None); L.gsr_debug_trace_emit(None)
         np.save(os.path.join(REPO, "gpurun_out", f"trace_bwd_cam{ci}.npy"), bbuf.cpu().numpy())
+        np.save(os.path.join(REPO, "gpurun_out", f"trace_fwd_cam{ci}.npy"), fbuf.cpu().numpy())
         report[ci] = {"emit": analyse_emit(ebuf.cpu().numpy(), f"cam{ci} emit"),
                       "fwd": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd"),
                       "bwd": analyse(bbuf.cpu().numpy(), 16 * T, f"cam{ci} bwd")}
