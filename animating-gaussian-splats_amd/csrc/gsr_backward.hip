@@ -91,7 +91,19 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 // transmittance T and front colour C_f, so the colour behind, projected on dL/dpixel, is
 // AR = (<dL/dpix, C_all - C_f> + T_final <bg, dL/dpix>) / T -- otherwise the pixel's final state
 // (T_final, AR = <bg, dL/dpix>).
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_render_bwd(
+#ifndef GSR_BWD_WPE
+#define GSR_BWD_WPE 6  // waves per SIMD the register budget is held to (0: compiler's choice)
+#endif
+#if GSR_BWD_WPE
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_BWD_WPE, 8)))
+#else
+#define GSR_BWD_ATTR
+#endif
+#ifndef GSR_BWD_WAVES
+#define GSR_BWD_WAVES 4  // items (one wave each) per workgroup
+#endif
+constexpr int kBwdWaves = GSR_BWD_WAVES;
+__global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
     const float4 *__restrict__ rec, const float *__restrict__ bg, const float4 *__restrict__ pix_end,
@@ -99,14 +111,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
     const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
     float4 *__restrict__ part) {
-    __shared__ float4 s_a[64], s_b[64], s_c[64];
-    __shared__ float s_out[64 * kPartial];  // per staged pair: its kPartial wave sums
-    if (blockIdx.x >= items[0].x) return;  // the launch covers the item bound
+    // Each wave of the workgroup takes its own item and its own LDS slice; the waves never
+    // synchronise with each other.  Items are in descending cost order, so the kBwdWaves items of
+    // one workgroup cost about the same: grouping them keeps the launch's workgroups coarse, which
+    // leaves the CUs' free slots to the forward kernels of the other streams in a pipelined step
+    // (one-wave workgroups take every slot a finishing wave frees and starve their large-LDS
+    // workgroups).
+    __shared__ float4 s_a_all[64 * kBwdWaves], s_b_all[64 * kBwdWaves], s_c_all[64 * kBwdWaves];
+    __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t item = blockIdx.x * kBwdWaves + wv;
+    if (item >= items[0].x) return;  // the launch covers the item bound
+    float4 *s_a = s_a_all + 64 * wv, *s_b = s_b_all + 64 * wv, *s_c = s_c_all + 64 * wv;
+    float *s_out = s_out_all + 64 * kPartial * wv;
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t tr_evals = 0, tr_reds = 0;  // (pair, quarter) evaluations and wave reductions
 #endif
-    const uint2 it = items[1 + blockIdx.x];
+    const uint2 it = items[1 + item];
     const int tile = (int)it.x;
     const uint32_t seg = it.y;
     const uint2 rg = ranges[tile];
@@ -185,6 +207,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
     // the batch ending at `e` (slots [max(e - 64, s0), e)): lane j's slot, its Gaussian's whole render
     // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
     // behind the current batch's pairs
+#if GSR_BWD_RECPF
+    // the batch ending at `e` (slots [max(e - 64, s0), e)): lane j's slot, its Gaussian's whole render
+    // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
+    // behind the current batch's pairs
+    float4 a_n = make_float4(0.f, 0.f, 0.f, 0.f), b_n = a_n, c_n = a_n, cj_n = a_n;
+    uint32_t em_n = 0;
+    auto fetch = [&](int e) {
+        const int st = e - 64 > s0 ? e - 64 : s0;
+        if (lane < e - st) {
+            const uint32_t g = point_list[rg.x + st + lane];
+            em_n = slot_emit[rg.x + st + lane];
+            const float4 *r = rec + (size_t)kRecF4 * g;
+            a_n = r[0]; b_n = r[1]; c_n = r[2]; cj_n = r[3];
+        }
+    };
+#else
     // the point list entry of each batch's slot is loaded one batch ahead (the render record gathers
     // depend on it); the records themselves are gathered at the batch start
     uint32_t g_n = 0, em_n = 0;
@@ -195,16 +233,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
             em_n = slot_emit[rg.x + st + lane];
         }
     };
+#endif
     if (s1 > s0) fetch(s1);
     for (int end = s1; end > s0; end -= 64) {
         const int start = end - 64 > s0 ? end - 64 : s0;
         const int cnt = end - start;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, cj = a;
         const uint32_t em = em_n;
+#if GSR_BWD_RECPF
+        const float4 a = a_n, b = b_n, c = c_n, cj = cj_n;
+#else
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, cj = a;
         if (lane < cnt) {
             const float4 *r = rec + (size_t)kRecF4 * g_n;
             a = r[0]; b = r[1]; c = r[2]; cj = r[3];  // cj: exact conic (a, b, c) of the staged Gaussian
         }
+#endif
         if (end - 64 > s0) fetch(end - 64);
 #pragma unroll
         for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
@@ -311,7 +354,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) void
         }
     }
 #ifdef GSR_TRACE
-    trace_wave(g_trace_bwd, blockIdx.x, t_start, tr_evals | ((uint64_t)tr_reds << 32));
+    trace_wave(g_trace_bwd, item, t_start, tr_evals | ((uint64_t)tr_reds << 32));
 #endif
 }
 
@@ -743,8 +786,9 @@ hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
 
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     if (a.K == 0) return hipSuccess;
-    // one wave per item; the launch covers the item bound, waves without an item exit at once
-    k_render_bwd<<<a.max_items, 64, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
+    // one wave per item, kBwdWaves per workgroup; the launch covers the item bound, waves without an
+    // item exit at once
+    k_render_bwd<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
                                              a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
                                              a.slot_emit, a.dL_dcolor, a.part);
     return hipGetLastError();
