@@ -92,12 +92,15 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 // AR = (<dL/dpix, C_all - C_f> + T_final <bg, dL/dpix>) / T -- otherwise the pixel's final state
 // (T_final, AR = <bg, dL/dpix>).
 #ifndef GSR_BWD_WPE
-#define GSR_BWD_WPE 6  // waves per SIMD the register budget is held to (0: compiler's choice)
+#define GSR_BWD_WPE 5  // waves per SIMD the register budget is held to (0: compiler's choice)
 #endif
 #if GSR_BWD_WPE
 #define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_BWD_WPE, 8)))
 #else
 #define GSR_BWD_ATTR
+#endif
+#ifndef GSR_BWD_ANY
+#define GSR_BWD_ANY 1  // skip the wave reduction of pairs no pixel of the wave took (0: always reduce)
 #endif
 #ifndef GSR_BWD_WAVES
 #define GSR_BWD_WAVES 4  // items (one wave each) per workgroup
@@ -324,7 +327,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             tr_evals += __builtin_popcount(qm);
             tr_reds += __ballot(any) ? 1u : 0u;
 #endif
-            if (__ballot(any)) {
+            if (!GSR_BWD_ANY || __ballot(any)) {
                 // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
                 const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
                 if ((lane & 15) < 2) {  // lanes 0 and 1 of each row hold the two halves of its sums:

@@ -54,7 +54,10 @@ struct GeomLayout {
 };
 
 // Binning work decomposition over Gaussians: NB chunks of CH Gaussians (CH multiple of 256).
-constexpr int kBinThreads = 1024;  // threads per binning block (one chunk of CH Gaussians)
+#ifndef GSR_BIN_THREADS
+#define GSR_BIN_THREADS 1024
+#endif
+constexpr int kBinThreads = GSR_BIN_THREADS;  // threads per binning block (one chunk of CH Gaussians)
 struct BinGrid {
     int CH, NB;
     __host__ __device__ BinGrid(int P) {
