@@ -330,9 +330,25 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
         }
         __syncthreads();
         GSR_EMIT_STAMP(1);
-        for (int t = threadIdx.x; t < T; t += blockDim.x) {
-            const uint32_t c = s_cur[t];
-            s_cur[t] = c ? atomicAdd(&tile_cursor[t], c) : 0u;
+        // reserve the slabs: every thread's (up to kReserveBatch) returning global atomics are issued
+        // before any result is consumed, so their device-scope round trips overlap instead of
+        // queueing one behind another
+        constexpr int kReserveBatch = 8;
+        for (int t0 = threadIdx.x; t0 < T; t0 += kReserveBatch * (int)blockDim.x) {
+            uint32_t c[kReserveBatch], r[kReserveBatch];
+#pragma unroll
+            for (int i = 0; i < kReserveBatch; ++i) {
+                const int t = t0 + i * (int)blockDim.x;
+                c[i] = t < T ? s_cur[t] : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < kReserveBatch; ++i)
+                r[i] = c[i] ? atomicAdd(&tile_cursor[t0 + i * (int)blockDim.x], c[i]) : 0u;
+#pragma unroll
+            for (int i = 0; i < kReserveBatch; ++i) {
+                const int t = t0 + i * (int)blockDim.x;
+                if (t < T) s_cur[t] = r[i];
+            }
         }
         __syncthreads();
         GSR_EMIT_STAMP(2);

@@ -38,9 +38,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh): HBM bytes per
 # launch of each kernel, converted per access shape (calibrated_traffic; MI355X_MICROARCH.md's 2 x
 # FETCH_SIZE + WRITE_SIZE is the streaming case and is reported beside it)
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01_hbm_pmc.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r02_hbm_pmc.json")
 # SQ counters of the same command (tools/profile_round.sh sq passes): VALU activity per launch
-SQ_SUMMARY = os.path.join(REPO, "profiles", "r01_sq_pmc.json")
+SQ_SUMMARY = os.path.join(REPO, "profiles", "r02_sq_pmc.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
 PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "bwd_items",
           "render_bwd", "gauss_bwd"]
@@ -722,6 +722,10 @@ def main():
                     "achieved_Ginst_s": round(rate, 1), "peak_Ginst_s": VALU_PEAK_GINST,
                     "issue_frac": round(rate / VALU_PEAK_GINST, 4),
                     "source": os.path.relpath(SQ_SUMMARY, REPO)}
+            if q.get("clock_ghz"):  # GRBM_GUI_ACTIVE / 8 / duration in the profile pass: the clock held
+                pk = 1024 * q["clock_ghz"] / 2  # Ginst/s at that clock
+                valu["profile_clock_ghz"] = round(q["clock_ghz"], 3)
+                valu["issue_frac_at_profile_clock"] = round(rate / pk, 4)
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, SH)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3

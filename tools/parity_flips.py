@@ -1,0 +1,37 @@
+"""Summarise gpurun_out/parity_stats.json (written by tests/test_gpu_parity.py on the GPU box) into a
+profiles/ record: per test, the fraction of values outside the 1e-4 tolerance for each compared
+quantity (the blend-threshold flips of DESIGN.md section 3) and the worst pixel / gradient rates.
+usage: python tools/parity_flips.py gpurun_out/parity_stats.json profiles/r02_parity_flips.json"""
+import json
+import sys
+from collections import OrderedDict
+
+PIXEL = {"n_contrib", "final_T", "color", "depth", "rgb"}
+
+
+def main():
+    rows = json.load(open(sys.argv[1]))
+    tests = OrderedDict()
+    for r in rows:
+        test, qty, frac = r[0].split("::")[-1], r[1], r[2]
+        if qty == "num_rendered":  # informational entries (K of the baseline views)
+            tests.setdefault("test_baseline_size_parity[%s]" % test, OrderedDict()).setdefault("info", {})[qty] = int(frac)
+            continue
+        t = tests.setdefault(test, OrderedDict())
+        t.setdefault("outside_tol", {})[qty] = frac
+        t.setdefault("worst_abs", {})[qty] = r[3]
+    for t in tests.values():
+        o = t.get("outside_tol", {})
+        t["max_pixel_frac"] = max([v for k, v in o.items() if k in PIXEL] or [0.0])
+        t["max_grad_frac"] = max([v for k, v in o.items() if k not in PIXEL] or [0.0])
+    out = {"source": "tests/test_gpu_parity.py (-m gpu) -> gpurun_out/parity_stats.json",
+           "tolerance": "1e-4 rel + 1e-6*max (image) / 1e-5*max (gradients); allowance <= 1e-4 of pixels, <= 1e-3 of gradient values",
+           "tests": tests}
+    json.dump(out, open(sys.argv[2], "w"), indent=1)
+    for k, t in tests.items():
+        if "max_pixel_frac" in t:
+            print(f"{k:<50} pixels {t['max_pixel_frac']:.1e}  gradients {t['max_grad_frac']:.1e}")
+
+
+if __name__ == "__main__":
+    main()

@@ -86,8 +86,12 @@ def sq(dirs):
         o = {c: sum(x) / len(x) for c, x in v.items()}
         if dur.get(k):
             o["avg_us_in_pass"] = sum(dur[k]) / len(dur[k])
+            if "GRBM_GUI_ACTIVE" in o:  # summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)
+                o["clock_ghz"] = o["GRBM_GUI_ACTIVE"] / 8 / (o["avg_us_in_pass"] * 1e-6) / 1e9
             if "SQ_INSTS_VALU" in o:
                 o["valu_issue_frac"] = o["SQ_INSTS_VALU"] * 2 / (1024 * o["avg_us_in_pass"] * 1e-6 * 2.4e9)
+                if "clock_ghz" in o:  # the same at the clock the chip held during the launch
+                    o["valu_issue_frac_at_clock"] = o["SQ_INSTS_VALU"] * 2 / (1024 * o["avg_us_in_pass"] * 1e-6 * o["clock_ghz"] * 1e9)
         out[k] = o
     return out
 
