@@ -649,20 +649,24 @@ __device__ inline bool tile_cull(float gx, float gy, float a, float b, float c, 
     const float dxlo = gx - x1, dxhi = gx - x0;
     const float dylo = gy - y1, dyhi = gy - y0;
     if (dxlo <= 0.f && dxhi >= 0.f && dylo <= 0.f && dyhi >= 0.f) return false;  // centre inside
+    // Each edge's minimiser uses the hardware reciprocal (1 ulp) instead of an IEEE division: a
+    // slightly-off minimiser inside the clamp range can only RAISE the edge value, by O(c ddy^2),
+    // ~1e-14 relative -- far inside the margin below, so the cull stays conservative.
+    const float ia = __builtin_amdgcn_rcpf(a), ic = __builtin_amdgcn_rcpf(c);
     float qmin;
     {   // edges with dx fixed: minimise over dy
         float dx = dxlo;
-        float dy = fminf(fmaxf(-b * dx / c, dylo), dyhi);
+        float dy = fminf(fmaxf(-b * dx * ic, dylo), dyhi);
         qmin = a * dx * dx + 2.f * b * dx * dy + c * dy * dy;
         dx = dxhi;
-        dy = fminf(fmaxf(-b * dx / c, dylo), dyhi);
+        dy = fminf(fmaxf(-b * dx * ic, dylo), dyhi);
         qmin = fminf(qmin, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
         // edges with dy fixed: minimise over dx
         dy = dylo;
-        dx = fminf(fmaxf(-b * dy / a, dxlo), dxhi);
+        dx = fminf(fmaxf(-b * dy * ia, dxlo), dxhi);
         qmin = fminf(qmin, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
         dy = dyhi;
-        dx = fminf(fmaxf(-b * dy / a, dxlo), dxhi);
+        dx = fminf(fmaxf(-b * dy * ia, dxlo), dxhi);
         qmin = fminf(qmin, a * dx * dx + 2.f * b * dx * dy + c * dy * dy);
     }
     return qmin > tau * 1.001f + 1e-3f;
