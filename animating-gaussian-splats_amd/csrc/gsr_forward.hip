@@ -750,10 +750,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
             const Blend e = blend_eval(a, b, pfx, pfy);
             const bool ok = !done && blend_ok(e);
-            const float test_T = Tt * (1.f - e.alpha);
-            const bool fin = ok && test_T < 0.0001f;
-            const bool use = ok && !fin;
-            done = done || fin;
+            const float test_T = fmaf(-e.alpha, Tt, Tt);  // T (1 - alpha), one rounding
+            // keep == !(test_T < 1e-4) (test_T is never NaN: T in (0, 1], alpha in [0, 0.99]); the
+            // pixel finishes when it takes the entry but may not keep it: (done | ok) & ~use, one
+            // compare and mask logic instead of a second compare
+            const bool use = ok && test_T >= 0.0001f;
+            done = (done || ok) && !use;
             const float w = use ? e.alpha * Tt : 0.f;
             C0 = fmaf(c.x, w, C0);
             C1 = fmaf(c.y, w, C1);
