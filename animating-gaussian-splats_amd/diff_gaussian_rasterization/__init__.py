@@ -39,17 +39,37 @@ class GaussianRasterizationSettings(NamedTuple):
     debug: bool = False
 
 
-def _engine_accumulates(t):
+def _engine_accumulates(t, node=None):
     """True when the running backward pass will execute ``t``'s AccumulateGrad node, i.e. write
     ``t.grad``: ``loss.backward()`` does; ``torch.autograd.grad(...)`` never does (the engine refuses
-    the query for its inputs) and ``loss.backward(inputs=[...])`` only for the listed leaves."""
+    the query for its inputs) and ``loss.backward(inputs=[...])`` only for the listed leaves.
+    ``node``: that AccumulateGrad node when the caller already has it (``_input_nodes``)."""
     try:
-        return bool(torch._C._will_engine_execute_node(get_gradient_edge(t).node))
+        return bool(torch._C._will_engine_execute_node(node if node is not None else get_gradient_edge(t).node))
     except RuntimeError:  # autograd.grad(): the gradient is returned, .grad is left alone
         return False
 
 
-def _accumulation_target(t):
+def _tensor_positions(args):
+    """Input index -> position in the Function node's ``next_functions`` (tensor inputs only)."""
+    pos, k = {}, 0
+    for i, a in enumerate(args):
+        if isinstance(a, torch.Tensor):
+            pos[i] = k
+            k += 1
+    return pos
+
+
+def _input_nodes(ctx, inputs):
+    """The graph edges of the given input indices, read off the backward node itself: for a leaf
+    that requires grad, its AccumulateGrad node (``get_gradient_edge(t).node``, ~8 us per call,
+    would cost ~50 us per backward on the host thread that feeds the GPU)."""
+    nf = ctx.next_functions
+    pos = ctx.tensor_pos
+    return [nf[pos[i]][0] if i in pos and pos[i] < len(nf) else None for i in inputs]
+
+
+def _accumulation_target(t, node=None):
     """The leaf's existing ``.grad`` when the backward kernel may add into it in place (and the
     Function then returns None for it): a leaf requiring grad whose gradient is a contiguous fp32
     tensor of its shape, with no hooks that autograd's accumulation would have run, in a backward
@@ -64,7 +84,7 @@ def _accumulation_target(t):
         return None
     if t._backward_hooks or getattr(t, "_post_accumulate_grad_hooks", None):
         return None
-    if torch.is_grad_enabled() or not _engine_accumulates(t):
+    if torch.is_grad_enabled() or not _engine_accumulates(t, node):
         return None
     return g
 
@@ -89,6 +109,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
         ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
+        ctx.tensor_pos = _tensor_positions((means3D, means2D, sh, colors_precomp, opacities, scales,
+                                            rotations, cov3Ds_precomp))
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
@@ -105,11 +127,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                 sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
-        acc = [_accumulation_target(t) if need else None
-               for t, need in zip(ctx.leaves, (ctx.needs_input_grad[1], ctx.needs_input_grad[3],
-                                               ctx.needs_input_grad[4], ctx.needs_input_grad[0],
-                                               ctx.needs_input_grad[7], ctx.needs_input_grad[2],
-                                               ctx.needs_input_grad[5], ctx.needs_input_grad[6]))]
+        inputs = (1, 3, 4, 0, 7, 2, 5, 6)  # input index of each leaf (grad output order)
+        acc = [_accumulation_target(t, node) if ctx.needs_input_grad[i] else None
+               for t, i, node in zip(ctx.leaves, inputs, _input_nodes(ctx, inputs))]
         g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc))
         for k, t in enumerate(acc):
             if t is not None:
@@ -191,6 +211,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         ctx.opacity_shape = opacity_logits.shape
         ctx.leaves = (means2D, colors, opacity_logits, means, None, sh, log_scales, quaternions)
+        ctx.tensor_pos = _tensor_positions((means, means2D, sh, colors, opacity_logits, log_scales, quaternions))
         ctx.save_for_backward(colors, means, log_scales, quaternions, radii, sh, geomBuffer,
                               binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii)
@@ -206,8 +227,11 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
             ctx.saved_tensors
         empty = torch.empty(0, device=means.device)
         need = ctx.needs_input_grad
-        acc = [_accumulation_target(t) if n else None
-               for t, n in zip(ctx.leaves, (need[1], need[3], need[4], need[0], False, need[2], need[5], need[6]))]
+        inputs = (1, 3, 4, 0, None, 2, 5, 6)  # input index of each leaf (grad output order; no cov3D)
+        nodes = _input_nodes(ctx, [i for i in inputs if i is not None])
+        nodes.insert(4, None)
+        acc = [_accumulation_target(t, node) if i is not None and need[i] else None
+               for t, i, node in zip(ctx.leaves, inputs, nodes)]
         if acc[2] is not None and acc[2].shape != (means.shape[0], 1):
             acc[2] = None
         (g_means2D, g_colors, g_opacity, g_means, _g_cov3D, g_sh, g_scales, g_rot) = \

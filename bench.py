@@ -472,6 +472,10 @@ def main():
                     help="HIP streams the step's views alternate over: one view's memory-bound "
                          "per-Gaussian backward overlaps the next view's VALU-bound render kernels; "
                          "libgsr orders the gradient writes across streams (bitwise the 1-stream result)")
+    ap.add_argument("--submit", default="serial", choices=["threads", "serial"],
+                    help="threads: one host thread per stream submits that stream's views, so a forward "
+                         "waiting for its num_rendered read-back blocks only its own thread and the other "
+                         "streams' views keep the GPU fed; serial: one thread submits every view in turn")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path on one GPU)")
@@ -571,15 +575,32 @@ def main():
     if reducer is not None:  # the bucket's zeroing (main stream) precedes the first backward
         _C.grad_fence(*grads_of())
 
+    pool = None
+    if args.submit == "threads" and len(streams) > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(max_workers=len(streams))
+
+    def run_views(vs, s):  # one stream's share of a step, fwd + bwd per view
+        torch.cuda.set_device(dev)
+        with torch.cuda.stream(s):
+            for ci in vs:
+                img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
+                img.backward(dl)
+
     def step(it):
         # No stream waits for another at the step start: libgsr orders the gradient writes across
         # streams, record_stream keeps freed gradients from early reuse, and for N > 1 the bucket's
         # all-reduce + reset on the main stream is declared with grad_fence, so the next step's
         # forwards run during the all-reduce and only its first gradient write waits for it.
-        for k, ci in enumerate(views_of(it)):
-            with torch.cuda.stream(streams[k % len(streams)]):
-                img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
-                img.backward(dl)
+        vs = views_of(it)
+        ns = len(streams)
+        if pool is not None:  # view k on stream k % ns, submitted by that stream's thread
+            futs = [pool.submit(run_views, vs[k::ns], streams[k]) for k in range(min(ns, len(vs)))]
+            for f in futs:
+                f.result()
+        else:
+            for k, ci in enumerate(vs):
+                run_views([ci], streams[k % ns])
         if reducer is not None:
             for s in streams:
                 main_stream.wait_stream(s)
@@ -764,6 +785,7 @@ def main():
                        "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
                        "mean_num_rendered": int(K), "max_tile_pairs": max_tile, "parallelism": f"camera-dp{world}" if args.config != "C5"
                        else f"frame-dp{world}", "streams_per_gpu": len(streams),
+                       "submission": "one host thread per stream" if pool is not None else "one host thread",
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
