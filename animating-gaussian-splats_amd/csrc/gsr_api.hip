@@ -330,28 +330,22 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     return GSR_OK;
 }
 
-int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
-                 const void *geom, const void *binning, const void *image, const float *dL_dcolor,
-                 const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
-                 void *stream) {
-    (void)dL_ddepth;
-    HostPhase host_total("host_backward");
-    int rc = check_common(cam, g, false);
-    if (rc) return rc;
-    if (!out) return fail(GSR_ERR_ARG, "gsr_backward: null grads");
-    if (g->P == 0) return GSR_OK;
+}  // extern "C"
+
+namespace {
+// The per-pixel half of the backward (bwd items + k_render_bwd): BwdArgs of the view and its SCRATCH
+// buffer (records at a.part) requested through `alloc`.
+int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
+                    const void *geom, const void *binning, const void *image, const float *dL_dcolor,
+                    gsr_alloc_fn alloc, void *alloc_ctx, hipStream_t s, BwdArgs &a) {
     if (!geom || !binning || !image || !dL_dcolor || !radii || !alloc)
         return fail(GSR_ERR_ARG, "gsr_backward: missing saved buffers / dL_dcolor / allocator");
-    if (!out->dL_dmeans2D || !out->dL_dopacity || !out->dL_dmeans3D || (g->shs && !out->dL_dsh))
-        return fail(GSR_ERR_ARG, "gsr_backward: missing gradient output");
     if (num_rendered < 0) return fail(GSR_ERR_ARG, "num_rendered < 0");
-    hipStream_t s = (hipStream_t)stream;
     FwdArgs f;
     fill_common(f, cam, g);
     carve_geom(f, (char *)geom);
     carve_image(f, (char *)image);
     carve_binning(f, (char *)binning, num_rendered);
-    BwdArgs a;
     memset(&a, 0, sizeof(a));
     a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
     a.act = f.act;
@@ -366,11 +360,6 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.seg_off = f.seg_off; a.meta = f.meta;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
     a.dL_dcolor = dL_dcolor;
-    a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
-    a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = out->dL_dsh;
-    a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
-    if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward: unknown accumulate bits 0x%x", out->accumulate);
-    a.accm = out->accumulate;
     const ScratchLayout SL(num_rendered, a.gx * a.gy);
     char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, SL.total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
@@ -379,9 +368,103 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
     { Phase ph(s, "bwd_items"); HIP_TRY(launch_bwd_items(a, s)); }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
+    return GSR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
+                 const void *geom, const void *binning, const void *image, const float *dL_dcolor,
+                 const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
+                 void *stream) {
+    (void)dL_ddepth;
+    HostPhase host_total("host_backward");
+    int rc = check_common(cam, g, false);
+    if (rc) return rc;
+    if (!out) return fail(GSR_ERR_ARG, "gsr_backward: null grads");
+    if (g->P == 0) return GSR_OK;
+    if (!out->dL_dmeans2D || !out->dL_dopacity || !out->dL_dmeans3D || (g->shs && !out->dL_dsh))
+        return fail(GSR_ERR_ARG, "gsr_backward: missing gradient output");
+    if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward: unknown accumulate bits 0x%x", out->accumulate);
+    hipStream_t s = (hipStream_t)stream;
+    BwdArgs a;
+    rc = backward_render(cam, g, radii, num_rendered, geom, binning, image, dL_dcolor, alloc, alloc_ctx, s, a);
+    if (rc) return rc;
+    a.dL_dmeans2D = out->dL_dmeans2D; a.dL_dcolors = out->dL_dcolors; a.dL_dopacity = out->dL_dopacity;
+    a.dL_dmeans3D = out->dL_dmeans3D; a.dL_dcov3D = out->dL_dcov3D; a.dL_dsh = out->dL_dsh;
+    a.dL_dscales = out->dL_dscales; a.dL_drot = out->dL_drotations;
+    a.accm = out->accumulate;
     const void *written[8] = {a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity, a.dL_dmeans3D,
                               a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot};
     { Phase ph(s, "gauss_bwd"); HIP_TRY(ordered_grad_write(written, 8, s, [&] { return launch_gauss_bwd(a, s); })); }
+    return GSR_OK;
+}
+
+int gsr_backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
+                        const void *geom, const void *binning, const void *image, const float *dL_dcolor,
+                        gsr_alloc_fn alloc, void *alloc_ctx, void *stream) {
+    HostPhase host_total("host_backward");
+    int rc = check_common(cam, g, false);
+    if (rc) return rc;
+    if (g->P == 0) return GSR_OK;
+    BwdArgs a;
+    return backward_render(cam, g, radii, num_rendered, geom, binning, image, dL_dcolor, alloc, alloc_ctx,
+                           (hipStream_t)stream, a);
+}
+
+int gsr_backward_gaussians(int nviews, const gsr_view_grad *views, const gsr_gaussians *g, gsr_grads *out,
+                           void *stream) {
+    HostPhase host_total("host_backward");
+    if (nviews < 0 || (nviews > 0 && !views) || !out) return fail(GSR_ERR_ARG, "gsr_backward_gaussians: bad view list / grads");
+    if (nviews == 0) return GSR_OK;
+    for (int v = 0; v < nviews; ++v) {
+        const int rc = check_common(views[v].cam, g, false);
+        if (rc) return rc;
+    }
+    if (g->P == 0) return GSR_OK;
+    if (g->shs && g->sh_coeffs != 1 && g->sh_coeffs != 4 && g->sh_coeffs != 9 && g->sh_coeffs != 16)
+        return fail(GSR_ERR_UNSUPPORTED, "gsr_backward_gaussians: %d SH coefficients (1, 4, 9 or 16 supported)", g->sh_coeffs);
+    if (!out->dL_dopacity || !out->dL_dmeans3D || (g->shs && !out->dL_dsh))
+        return fail(GSR_ERR_ARG, "gsr_backward_gaussians: missing gradient output");
+    if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward_gaussians: unknown accumulate bits 0x%x", out->accumulate);
+    for (int v = 0; v < nviews; ++v)
+        if (!views[v].radii || !views[v].geom || !views[v].scratch || views[v].num_rendered < 0)
+            return fail(GSR_ERR_ARG, "gsr_backward_gaussians: view %d lacks radii / geom / scratch", v);
+    hipStream_t s = (hipStream_t)stream;
+    MultiArgs m;
+    memset(&m, 0, sizeof(m));
+    m.P = g->P; m.D = g->sh_degree; m.M = g->shs ? g->sh_coeffs : 0; m.act = g->activations;
+    m.scale_modifier = g->scale_modifier;
+    m.means3D = g->means3D; m.scales = g->scales; m.rotations = g->rotations; m.shs = g->shs;
+    m.cov3D_precomp = g->cov3D_precomp;
+    m.dL_dcolors = out->dL_dcolors; m.dL_dopacity = out->dL_dopacity; m.dL_dmeans3D = out->dL_dmeans3D;
+    m.dL_dcov3D = out->dL_dcov3D; m.dL_dsh = out->dL_dsh; m.dL_dscales = out->dL_dscales; m.dL_drot = out->dL_drotations;
+    for (int v0 = 0; v0 < nviews; v0 += kMultiViews) {  // groups of kMultiViews views; later groups add
+        m.nv = std::min(kMultiViews, nviews - v0);
+        m.accm = (out->accumulate | (v0 ? 0xFF : 0)) & ~GSR_GRAD_MEANS2D;
+        const void *written[8 + kMultiViews] = {m.dL_dcolors, m.dL_dopacity, m.dL_dmeans3D, m.dL_dcov3D,
+                                                m.dL_dsh, m.dL_dscales, m.dL_drot};
+        for (int k = 0; k < m.nv; ++k) {
+            const gsr_view_grad &vg = views[v0 + k];
+            const gsr_camera *cam = vg.cam;
+            FwdArgs f;
+            fill_common(f, cam, g);
+            MultiView &mv = m.v[k];
+            mv.viewmatrix = cam->viewmatrix; mv.projmatrix = cam->projmatrix; mv.campos = cam->campos;
+            mv.cs = f.cs;
+            mv.tan_fovx = f.tan_fovx; mv.tan_fovy = f.tan_fovy; mv.focal_x = f.focal_x; mv.focal_y = f.focal_y;
+            mv.radii = vg.radii;
+            mv.goff = (const uint32_t *)((const char *)vg.geom + GeomLayout(g->P).goff);
+            mv.rec = (const float4 *)((const char *)vg.geom + GeomLayout(g->P).rec);
+            mv.part = (const float4 *)((const char *)vg.scratch +
+                                       ScratchLayout(vg.num_rendered, f.gx * f.gy).part);
+            mv.dL_dmeans2D = vg.dL_dmeans2D;
+            mv.acc2 = vg.accumulate_means2D ? 1 : 0;
+            written[7 + k] = vg.dL_dmeans2D;
+        }
+        { Phase ph(s, "gauss_bwd"); HIP_TRY(ordered_grad_write(written, 7 + m.nv, s, [&] { return launch_gauss_bwd_multi(m, s); })); }
+    }
     return GSR_OK;
 }
 

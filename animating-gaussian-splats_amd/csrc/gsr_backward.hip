@@ -386,14 +386,10 @@ __device__ inline float3 unit_vec_bwd(float3 v, float3 g) {
 // SH backward; writes all M coefficient rows of dL_dsh (zeros past the active degree).  `sh` and
 // `dL_dsh` may alias (the same LDS row): phase 1 reads the coefficients (direction derivative),
 // phase 2 writes the coefficient gradients, which depend only on the direction and dL/dRGB.
-template <typename ShPtr, typename OutPtr>
-__device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos, ShPtr sh,
-                                     const bool *clamped, float3 dL_dcolor, OutPtr dL_dsh, bool acc = false) {
-    const float3 d0 = make_float3(mean.x - campos.x, mean.y - campos.y, mean.z - campos.z);
-    const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
-    const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
-    const float dRGB[3] = {dL_dcolor.x * (clamped[0] ? 0.f : 1.f), dL_dcolor.y * (clamped[1] ? 0.f : 1.f),
-                           dL_dcolor.z * (clamped[2] ? 0.f : 1.f)};
+// Phase 1 alone: dL/d(direction) = sum_c dRGB_c d(RGB_c)/d(dir) from the coefficients (before the
+// normalisation's chain rule).  (x, y, z) = the unit direction.
+template <typename ShPtr>
+__device__ inline float3 sh_dir_grad(int deg, float x, float y, float z, ShPtr sh, const float (&dRGB)[3]) {
     const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
     float dx[3] = {0, 0, 0}, dy[3] = {0, 0, 0}, dz[3] = {0, 0, 0};
 #define SH(i, c) sh[(i) * 3 + (c)]
@@ -431,8 +427,14 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos,
         }
     }
 #undef SH
-    // ---- phase 2: coefficient gradients (basis value x dL/dRGB) ----
-    float basis[16];
+    return make_float3(dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2],
+                       dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
+                       dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]);
+}
+
+// The 16 SH basis values of the unit direction (x, y, z) (degree 3 and below).
+__device__ inline void sh_basis16(float x, float y, float z, float (&basis)[16]) {
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
     basis[0] = GSR_SH_C0;
     basis[1] = -GSR_SH_C1 * y; basis[2] = GSR_SH_C1 * z; basis[3] = -GSR_SH_C1 * x;
     basis[4] = kSH_C2[0] * xy; basis[5] = kSH_C2[1] * yz; basis[6] = kSH_C2[2] * (2.f * zz - xx - yy);
@@ -444,6 +446,23 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos,
     basis[13] = kSH_C3[4] * x * (4.f * zz - xx - yy);
     basis[14] = kSH_C3[5] * z * (xx - yy);
     basis[15] = kSH_C3[6] * x * (xx - 3.f * yy);
+}
+
+// The SH colour's derivative with respect to the mean (returned) and the coefficient gradients
+// (written to all M rows of dL_dsh, zeros past the active degree).  `sh` and `dL_dsh` may alias (the
+// same LDS row): phase 1 reads the coefficients (direction derivative), phase 2 writes the
+// coefficient gradients, which depend only on the direction and dL/dRGB.
+template <typename ShPtr, typename OutPtr>
+__device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos, ShPtr sh,
+                                     const bool *clamped, float3 dL_dcolor, OutPtr dL_dsh, bool acc = false) {
+    const float3 d0 = make_float3(mean.x - campos.x, mean.y - campos.y, mean.z - campos.z);
+    const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
+    const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
+    const float dRGB[3] = {dL_dcolor.x * (clamped[0] ? 0.f : 1.f), dL_dcolor.y * (clamped[1] ? 0.f : 1.f),
+                           dL_dcolor.z * (clamped[2] ? 0.f : 1.f)};
+    const float3 dL_ddir = sh_dir_grad(deg, x, y, z, sh, dRGB);
+    float basis[16];
+    sh_basis16(x, y, z, basis);
     const int active = (deg + 1) * (deg + 1);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -457,9 +476,6 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos,
     }
     for (int i = 16; i < M; ++i)
         for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] : 0.f;
-    const float3 dL_ddir = make_float3(dx[0] * dRGB[0] + dx[1] * dRGB[1] + dx[2] * dRGB[2],
-                                       dy[0] * dRGB[0] + dy[1] * dRGB[1] + dy[2] * dRGB[2],
-                                       dz[0] * dRGB[0] + dz[1] * dRGB[1] + dz[2] * dRGB[2]);
     return unit_vec_bwd(d0, dL_ddir);
 }
 
@@ -507,17 +523,17 @@ __device__ inline void cov3d_backward(float3 s3, float mod, float4 q, const floa
 // kRecChunk: 256 records when the SH rows' LDS slice of a wave holds them (MC = 16), else 128.
 template <int MC> constexpr int kRecChunk = 3 * 256 * 16 <= 64 * sh_row_stride(MC) * 4 ? 256 : 128;
 template <int MC> constexpr int kRecStageF4 = 3 * kRecChunk<MC>;  // float4 per wave slice
-template <int MC>
-__device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict__ goff,
-                                        const float4 *__restrict__ part, float4 *stage,
-                                        float (&acc)[kPartial]) {
+template <int C>  // records per staged chunk (the wave's LDS slice holds 3 C float4)
+__device__ inline void sum_records_chunked(int i, int P, const uint32_t *__restrict__ goff,
+                                           const float4 *__restrict__ part, float4 *stage,
+                                           float (&acc)[kPartial]) {
     const int lane = threadIdx.x & 63;
     const uint32_t e0 = goff[min(i, P)], e1 = goff[min(i + 1, P)];  // both in flight at once
     const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0);
     const uint32_t E1 = __builtin_amdgcn_readlane(e1, 63);
 #pragma unroll
     for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
-    constexpr int C = kRecChunk<MC>, NF4 = kRecStageF4<MC>;
+    constexpr int NF4 = 3 * C;
     for (uint32_t cb = E0; cb < E1; cb += C) {
         const uint32_t n3 = 3u * min((uint32_t)C, E1 - cb);
         const float4 *src = part + 3 * (size_t)cb;
@@ -538,6 +554,95 @@ __device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict
         }
         wave_lds_sync();
     }
+}
+template <int MC>
+__device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict__ goff,
+                                        const float4 *__restrict__ part, float4 *stage,
+                                        float (&acc)[kPartial]) {
+    sum_records_chunked<kRecChunk<MC>>(i, P, goff, part, stage, acc);
+}
+
+// dL/dconic (acc[2..4]) and dL/dmeans2D (acc[0..1]) of one view -> dL/dcov3D (dcov, upper triangle)
+// and the mean's gradient through the view's Jacobian and projection (dm): SURVEY.md 2.1 rows
+// computeCov2DCUDA + preprocessCUDA bwd (the SH and cov3D chains are the callers').
+__device__ inline void view_chain(float3 mean, const float (&c3)[6], const float (&vm)[16], const float (&pj)[16],
+                                  float tan_fovx, float tan_fovy, float h_x, float h_y,
+                                  const float (&acc)[kPartial], float (&dcov)[6], float &dm0, float &dm1,
+                                  float &dm2) {
+    const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
+    float3 t = xform4x3(mean, vm);
+    const float limx = 1.3f * tan_fovx, limy = 1.3f * tan_fovy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float keep_tx = txtz < -limx || txtz > limx ? 0 : 1;
+    const float keep_ty = tytz < -limy || tytz > limy ? 0 : 1;
+    const m3 J = {{h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
+                   -(h_y * t.y) / (t.z * t.z), 0, 0, 0}};
+    const m3 Wm = {{vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]}};
+    const m3 V = {{c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]}};
+    const m3 T = m3_mul(Wm, J);
+    const m3 c2 = m3_mul(m3_mul(m3_T(T), m3_T(V)), T);
+    const float a = GM(c2, 0, 0) + 0.3f, b = GM(c2, 0, 1), c = GM(c2, 1, 1) + 0.3f;
+    const float denom = a * c - b * b;
+    float dL_da = 0, dL_db = 0, dL_dc = 0;
+    const float inv_det2 = 1.0f / ((denom * denom) + 0.0000001f);
+#define TT(cc, rr) GM(T, cc, rr)
+    if (inv_det2 != 0) {
+        dL_da = inv_det2 * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
+        dL_dc = inv_det2 * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
+        dL_db = inv_det2 * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
+        dcov[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
+        dcov[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
+        dcov[5] = (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc);
+        dcov[1] = 2 * TT(0, 0) * TT(0, 1) * dL_da + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dL_db +
+                  2 * TT(1, 0) * TT(1, 1) * dL_dc;
+        dcov[2] = 2 * TT(0, 0) * TT(0, 2) * dL_da + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dL_db +
+                  2 * TT(1, 0) * TT(1, 2) * dL_dc;
+        dcov[4] = 2 * TT(0, 2) * TT(0, 1) * dL_da + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dL_db +
+                  2 * TT(1, 1) * TT(1, 2) * dL_dc;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dcov[k] = 0;
+    }
+#define VV(cc, rr) GM(V, cc, rr)
+    const float dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
+                       (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_db;
+    const float dT01 = 2 * (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_da +
+                       (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_db;
+    const float dT02 = 2 * (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_da +
+                       (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_db;
+    const float dT10 = 2 * (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_dc +
+                       (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_db;
+    const float dT11 = 2 * (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_dc +
+                       (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_db;
+    const float dT12 = 2 * (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_dc +
+                       (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_db;
+#undef TT
+#undef VV
+#define WW(cc, rr) GM(Wm, cc, rr)
+    const float dJ00 = WW(0, 0) * dT00 + WW(0, 1) * dT01 + WW(0, 2) * dT02;
+    const float dJ02 = WW(2, 0) * dT00 + WW(2, 1) * dT01 + WW(2, 2) * dT02;
+    const float dJ11 = WW(1, 0) * dT10 + WW(1, 1) * dT11 + WW(1, 2) * dT12;
+    const float dJ12 = WW(2, 0) * dT10 + WW(2, 1) * dT11 + WW(2, 2) * dT12;
+#undef WW
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dL_dtx = keep_tx * -h_x * tz2 * dJ02;
+    const float dL_dty = keep_ty * -h_y * tz2 * dJ12;
+    const float dL_dtz = -h_x * tz2 * dJ00 - h_y * tz2 * dJ11 + (2 * h_x * t.x) * tz3 * dJ02 +
+                         (2 * h_y * t.y) * tz3 * dJ12;
+    dm0 = vm[0] * dL_dtx + vm[1] * dL_dty + vm[2] * dL_dtz;
+    dm1 = vm[4] * dL_dtx + vm[5] * dL_dty + vm[6] * dL_dtz;
+    dm2 = vm[8] * dL_dtx + vm[9] * dL_dty + vm[10] * dL_dtz;
+    // ---- screen-space mean -> means3D through the projection ----
+    const float4 mh = xform4x4(mean, pj);
+    const float m_w = 1.0f / (mh.w + 0.0000001f);
+    const float mul1 = (pj[0] * mean.x + pj[4] * mean.y + pj[8] * mean.z + pj[12]) * m_w * m_w;
+    const float mul2 = (pj[1] * mean.x + pj[5] * mean.y + pj[9] * mean.z + pj[13]) * m_w * m_w;
+    const float g2x = acc[0], g2y = acc[1];
+    dm0 += (pj[0] * m_w - pj[3] * mul1) * g2x + (pj[1] * m_w - pj[3] * mul2) * g2y;
+    dm1 += (pj[4] * m_w - pj[7] * mul1) * g2x + (pj[5] * m_w - pj[7] * mul2) * g2y;
+    dm2 += (pj[8] * m_w - pj[11] * mul1) * g2x + (pj[9] * m_w - pj[11] * mul2) * g2y;
 }
 
 template <int MC>
@@ -600,8 +705,6 @@ __device__ inline void gauss_bwd_one(
             gput_old(dL_dcolors, 3 * i + 2, acc[8], ac, oc[2]);
         }
     }
-    const float dcx = acc[2], dcy = acc[3], dcz = acc[4];
-
     float vm[16], pj[16];
     load_mat16(viewmatrix, cs.v0, cs.v1, vm);
     load_mat16(projmatrix, cs.p0, cs.p1, pj);
@@ -620,85 +723,12 @@ __device__ inline void gauss_bwd_one(
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) { qn = quat_norm(q); q = act_normalize(q, qn); }
         cov3d_from_scale_rot(s3, scale_modifier, q, c3);
     }
-    // ---- dL/dconic -> dL/dSigma2D -> dL/dSigma3D, and the mean's share through J ----
-    float3 t = xform4x3(mean, vm);
-    const float limx = 1.3f * tan_fovx, limy = 1.3f * tan_fovy;
-    const float txtz = t.x / t.z, tytz = t.y / t.z;
-    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
-    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
-    const float keep_tx = txtz < -limx || txtz > limx ? 0 : 1;
-    const float keep_ty = tytz < -limy || tytz > limy ? 0 : 1;
-    const m3 J = {{h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
-                   -(h_y * t.y) / (t.z * t.z), 0, 0, 0}};
-    const m3 Wm = {{vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]}};
-    const m3 V = {{c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]}};
-    const m3 T = m3_mul(Wm, J);
-    const m3 c2 = m3_mul(m3_mul(m3_T(T), m3_T(V)), T);
-    const float a = GM(c2, 0, 0) + 0.3f, b = GM(c2, 0, 1), c = GM(c2, 1, 1) + 0.3f;
-    const float denom = a * c - b * b;
-    float dL_da = 0, dL_db = 0, dL_dc = 0;
-    const float inv_det2 = 1.0f / ((denom * denom) + 0.0000001f);
-    float dcov[6];
-#define TT(cc, rr) GM(T, cc, rr)
-    if (inv_det2 != 0) {
-        dL_da = inv_det2 * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
-        dL_dc = inv_det2 * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
-        dL_db = inv_det2 * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
-        dcov[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
-        dcov[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
-        dcov[5] = (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc);
-        dcov[1] = 2 * TT(0, 0) * TT(0, 1) * dL_da + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dL_db +
-                  2 * TT(1, 0) * TT(1, 1) * dL_dc;
-        dcov[2] = 2 * TT(0, 0) * TT(0, 2) * dL_da + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dL_db +
-                  2 * TT(1, 0) * TT(1, 2) * dL_dc;
-        dcov[4] = 2 * TT(0, 2) * TT(0, 1) * dL_da + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dL_db +
-                  2 * TT(1, 1) * TT(1, 2) * dL_dc;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dcov[k] = 0;
-    }
+    float dcov[6], dm0, dm1, dm2;
+    view_chain(mean, c3, vm, pj, tan_fovx, tan_fovy, h_x, h_y, acc, dcov, dm0, dm1, dm2);
     if (dL_dcov3D) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) gput(dL_dcov3D, 6 * i + k, dcov[k], acv);
     }
-#define VV(cc, rr) GM(V, cc, rr)
-    const float dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
-                       (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_db;
-    const float dT01 = 2 * (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_da +
-                       (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_db;
-    const float dT02 = 2 * (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_da +
-                       (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_db;
-    const float dT10 = 2 * (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_dc +
-                       (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_db;
-    const float dT11 = 2 * (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_dc +
-                       (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_db;
-    const float dT12 = 2 * (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_dc +
-                       (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_db;
-#undef TT
-#undef VV
-#define WW(cc, rr) GM(Wm, cc, rr)
-    const float dJ00 = WW(0, 0) * dT00 + WW(0, 1) * dT01 + WW(0, 2) * dT02;
-    const float dJ02 = WW(2, 0) * dT00 + WW(2, 1) * dT01 + WW(2, 2) * dT02;
-    const float dJ11 = WW(1, 0) * dT10 + WW(1, 1) * dT11 + WW(1, 2) * dT12;
-    const float dJ12 = WW(2, 0) * dT10 + WW(2, 1) * dT11 + WW(2, 2) * dT12;
-#undef WW
-    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-    const float dL_dtx = keep_tx * -h_x * tz2 * dJ02;
-    const float dL_dty = keep_ty * -h_y * tz2 * dJ12;
-    const float dL_dtz = -h_x * tz2 * dJ00 - h_y * tz2 * dJ11 + (2 * h_x * t.x) * tz3 * dJ02 +
-                         (2 * h_y * t.y) * tz3 * dJ12;
-    float dm0 = vm[0] * dL_dtx + vm[1] * dL_dty + vm[2] * dL_dtz;
-    float dm1 = vm[4] * dL_dtx + vm[5] * dL_dty + vm[6] * dL_dtz;
-    float dm2 = vm[8] * dL_dtx + vm[9] * dL_dty + vm[10] * dL_dtz;
-    // ---- screen-space mean -> means3D through the projection ----
-    const float4 mh = xform4x4(mean, pj);
-    const float m_w = 1.0f / (mh.w + 0.0000001f);
-    const float mul1 = (pj[0] * mean.x + pj[4] * mean.y + pj[8] * mean.z + pj[12]) * m_w * m_w;
-    const float mul2 = (pj[1] * mean.x + pj[5] * mean.y + pj[9] * mean.z + pj[13]) * m_w * m_w;
-    const float g2x = acc[0], g2y = acc[1];
-    dm0 += (pj[0] * m_w - pj[3] * mul1) * g2x + (pj[1] * m_w - pj[3] * mul2) * g2y;
-    dm1 += (pj[4] * m_w - pj[7] * mul1) * g2x + (pj[5] * m_w - pj[7] * mul2) * g2y;
-    dm2 += (pj[8] * m_w - pj[11] * mul1) * g2x + (pj[9] * m_w - pj[11] * mul2) * g2y;
     if (MC > 0) {
         bool cl[3];
         const float3 cp = load_campos(campos, cs.c0);
@@ -779,6 +809,184 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     }
 }
 
+// ---- the per-Gaussian backward of several views in one pass (gsr_backward_gaussians) -----------
+// A training step's views (train.py:753-767 sums 5 view losses before ONE backward) share every
+// parameter and gradient array: one thread per Gaussian reads its parameters and SH row once, walks
+// the views -- each view's records summed from its own SCRATCH (staged per wave as in k_gauss_bwd),
+// its cov2D / projection / SH chains with its own camera -- and keeps the running sums of the
+// per-Gaussian gradients in registers (dL/dcov3D is summed before the single cov3D -> scale /
+// rotation chain: that chain is linear in it), then adds them into the gradient arrays ONCE.
+// Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
+// read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
+// Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
+constexpr int kMultiChunk = 128;  // records per staged chunk (6 KB of LDS per wave)
+template <int MC>
+constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_stride(MC) + 3) & ~size_t(3)) : 0; }
+template <int MC>
+constexpr size_t multi_lds_bytes() {
+    return sizeof(float) * multi_sh_floats<MC>() + sizeof(float4) * 3 * kMultiChunk * (kShBlock / 64);
+}
+
+template <int MC>  // SH coefficient count (1, 4, 9, 16), or 0 without SH (colours precomputed)
+__global__ __launch_bounds__(kShBlock) void k_gauss_bwd_multi(const MultiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
+    float4 *stage = reinterpret_cast<float4 *>(s_sh + multi_sh_floats<MC>()) + (threadIdx.x >> 6) * (3 * kMultiChunk);
+    const int P = a.P;
+    const int i0 = blockIdx.x * kShBlock;
+    const int nrow = min(kShBlock, P - i0);
+    const int i = i0 + threadIdx.x;
+    const bool live = i < P;
+    const int ii = live ? i : i0;  // lanes past P load (and never store) row i0's parameters
+    float *s_row = s_sh + threadIdx.x * RS;
+    if constexpr (MC > 0) {  // coefficient rows, read by every view's SH chain
+        sh_rows_to_lds<MC>(a.shs + (size_t)i0 * RL, nrow, s_sh);
+        __syncthreads();
+    }
+    const float3 mean = make_float3(a.means3D[3 * ii], a.means3D[3 * ii + 1], a.means3D[3 * ii + 2]);
+    float c3[6];
+    float3 s3 = make_float3(0, 0, 0);
+    float4 q = make_float4(0, 0, 0, 0);
+    float qn = 0.f;
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3[k] = a.cov3D_precomp[6 * ii + k];
+    } else {
+        s3 = make_float3(a.scales[3 * ii], a.scales[3 * ii + 1], a.scales[3 * ii + 2]);
+        q = make_float4(a.rotations[4 * ii], a.rotations[4 * ii + 1], a.rotations[4 * ii + 2], a.rotations[4 * ii + 3]);
+        if (a.act & GSR_ACT_EXP_SCALES) s3 = act_exp3(s3);
+        if (a.act & GSR_ACT_NORMALIZE_ROTATIONS) { qn = quat_norm(q); q = act_normalize(q, qn); }
+        cov3d_from_scale_rot(s3, a.scale_modifier, q, c3);
+    }
+    float gm0 = 0.f, gm1 = 0.f, gm2 = 0.f, gop = 0.f, gc0 = 0.f, gc1 = 0.f, gc2 = 0.f;
+    float gcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float gsh[RL > 0 ? RL : 1];
+#pragma unroll
+    for (int k = 0; k < (RL > 0 ? RL : 1); ++k) gsh[k] = 0.f;
+    bool vis = false;
+    float o_act = 0.f;  // the activated opacity, from the record of a view that sees the Gaussian
+    const int active = (a.D + 1) * (a.D + 1);
+    for (int v = 0; v < a.nv; ++v) {
+        const MultiView &V = a.v[v];
+        float acc[kPartial];
+        sum_records_chunked<kMultiChunk>(i, P, V.goff, V.part, stage, acc);  // wave-collective
+        if (!live) continue;
+        const bool r = V.radii[i] > 0;
+        if (V.dL_dmeans2D) {
+            float o2[3];
+            old_load(V.dL_dmeans2D, 3 * (size_t)i, V.acc2, o2);
+            gput_old(V.dL_dmeans2D, 3 * i, r ? acc[0] : 0.f, V.acc2, o2[0]);
+            gput_old(V.dL_dmeans2D, 3 * i + 1, r ? acc[1] : 0.f, V.acc2, o2[1]);
+            gput_old(V.dL_dmeans2D, 3 * i + 2, 0.f, V.acc2, o2[2]);
+        }
+        if (!r) continue;
+        if (!vis) o_act = V.rec[(size_t)kRecF4 * i + 1].y;  // written by every view that sees it
+        vis = true;
+        gop += acc[5]; gc0 += acc[6]; gc1 += acc[7]; gc2 += acc[8];
+        float vm[16], pj[16];
+        load_mat16(V.viewmatrix, V.cs.v0, V.cs.v1, vm);
+        load_mat16(V.projmatrix, V.cs.p0, V.cs.p1, pj);
+        float dcov[6], dm0, dm1, dm2;
+        view_chain(mean, c3, vm, pj, V.tan_fovx, V.tan_fovy, V.focal_x, V.focal_y, acc, dcov, dm0, dm1, dm2);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) gcov[k] += dcov[k];
+        if constexpr (MC > 0) {
+            const float3 cp = load_campos(V.campos, V.cs.c0);
+            bool cl[3];
+            (void)sh_to_rgb(a.D, mean, cp, s_row, cl);  // the forward's clamp mask in this view
+            const float3 d0 = make_float3(mean.x - cp.x, mean.y - cp.y, mean.z - cp.z);
+            const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
+            const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
+            const float dRGB[3] = {acc[6] * (cl[0] ? 0.f : 1.f), acc[7] * (cl[1] ? 0.f : 1.f),
+                                   acc[8] * (cl[2] ? 0.f : 1.f)};
+            const float3 d = unit_vec_bwd(d0, sh_dir_grad(a.D, x, y, z, s_row, dRGB));
+            dm0 += d.x; dm1 += d.y; dm2 += d.z;
+            float basis[16];
+            sh_basis16(x, y, z, basis);
+#pragma unroll
+            for (int k = 0; k < MC; ++k)
+                if (k < active) {
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) gsh[3 * k + c] += basis[k] * dRGB[c];
+                }
+        }
+        gm0 += dm0; gm1 += dm1; gm2 += dm2;
+    }
+    if (live) {
+        const int accm = a.accm;
+        const bool ac = accm & GSR_GRAD_COLORS, ao = accm & GSR_GRAD_OPACITY, a3 = accm & GSR_GRAD_MEANS3D,
+                   acv = accm & GSR_GRAD_COV3D, asc = accm & GSR_GRAD_SCALES, ar = accm & GSR_GRAD_ROTATIONS;
+        if (!vis) {  // no view sees it: zero gradient, accumulated outputs keep their content
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (!a3) a.dL_dmeans3D[3 * i + k] = 0.f;
+                if (a.dL_dcolors && !ac) a.dL_dcolors[3 * i + k] = 0.f;
+                if (a.dL_dscales && !asc) a.dL_dscales[3 * i + k] = 0.f;
+            }
+            if (!ao) a.dL_dopacity[i] = 0.f;
+            if (a.dL_dcov3D && !acv) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * i + k] = 0.f;
+            }
+            if (a.dL_drot && !ar) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a.dL_drot[4 * i + k] = 0.f;
+            }
+        } else {
+            float oo[1], oc[3], o3[3];
+            old_load(a.dL_dopacity, (size_t)i, ao, oo);
+            old_load(a.dL_dcolors, 3 * (size_t)i, a.dL_dcolors && ac, oc);
+            old_load(a.dL_dmeans3D, 3 * (size_t)i, a3, o3);
+            if (a.act & GSR_ACT_SIGMOID_OPACITY) {  // d/dlogit = o (1 - o), o from a forward's record
+                gput_old(a.dL_dopacity, i, gop * ((1.f - o_act) * o_act), ao, oo[0]);
+            } else {
+                gput_old(a.dL_dopacity, i, gop, ao, oo[0]);
+            }
+            if (a.dL_dcolors) {
+                gput_old(a.dL_dcolors, 3 * i, gc0, ac, oc[0]); gput_old(a.dL_dcolors, 3 * i + 1, gc1, ac, oc[1]);
+                gput_old(a.dL_dcolors, 3 * i + 2, gc2, ac, oc[2]);
+            }
+            gput_old(a.dL_dmeans3D, 3 * i, gm0, a3, o3[0]); gput_old(a.dL_dmeans3D, 3 * i + 1, gm1, a3, o3[1]);
+            gput_old(a.dL_dmeans3D, 3 * i + 2, gm2, a3, o3[2]);
+            if (a.dL_dcov3D) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) gput(a.dL_dcov3D, 6 * i + k, gcov[k], acv);
+            }
+            const bool has_sr = a.scales && !a.cov3D_precomp;
+            if (has_sr) {
+                float os[3], orr[4];
+                old_load(a.dL_dscales, 3 * (size_t)i, a.dL_dscales && asc, os);
+                old_load(a.dL_drot, 4 * (size_t)i, a.dL_drot && ar, orr);
+                float3 ds; float4 dr;
+                cov3d_backward(s3, a.scale_modifier, q, gcov, ds, dr);
+                if (a.act & GSR_ACT_EXP_SCALES) { ds.x *= s3.x; ds.y *= s3.y; ds.z *= s3.z; }
+                if (a.act & GSR_ACT_NORMALIZE_ROTATIONS) dr = act_normalize_bwd(q, qn, dr);
+                if (a.dL_dscales) {
+                    gput_old(a.dL_dscales, 3 * i, ds.x, asc, os[0]); gput_old(a.dL_dscales, 3 * i + 1, ds.y, asc, os[1]);
+                    gput_old(a.dL_dscales, 3 * i + 2, ds.z, asc, os[2]);
+                }
+                if (a.dL_drot) {
+                    gput_old(a.dL_drot, 4 * i, dr.x, ar, orr[0]); gput_old(a.dL_drot, 4 * i + 1, dr.y, ar, orr[1]);
+                    gput_old(a.dL_drot, 4 * i + 2, dr.z, ar, orr[2]); gput_old(a.dL_drot, 4 * i + 3, dr.w, ar, orr[3]);
+                }
+            } else {
+                if (a.dL_dscales && !asc) { a.dL_dscales[3 * i] = 0.f; a.dL_dscales[3 * i + 1] = 0.f; a.dL_dscales[3 * i + 2] = 0.f; }
+                if (a.dL_drot && !ar) { a.dL_drot[4 * i] = 0.f; a.dL_drot[4 * i + 1] = 0.f; a.dL_drot[4 * i + 2] = 0.f; a.dL_drot[4 * i + 3] = 0.f; }
+            }
+        }
+    }
+    if constexpr (MC > 0) {  // the summed dL/dSH rows through LDS (over the coefficients), coalesced store
+        __syncthreads();
+        if (live) {
+#pragma unroll
+            for (int k = 0; k < RL; ++k) s_row[k] = gsh[k];
+        }
+        __syncthreads();
+        if (a.accm & GSR_GRAD_SH) sh_rows_from_lds<MC, true>(s_sh, nrow, a.dL_dsh + (size_t)i0 * RL);
+        else sh_rows_from_lds<MC, false>(s_sh, nrow, a.dL_dsh + (size_t)i0 * RL);
+    }
+}
+
 
 // ==========================================================================================
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
@@ -816,6 +1024,23 @@ hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {
         case 4: gauss_bwd_mc<4>(a, s); break;
         case 1: gauss_bwd_mc<1>(a, s); break;
         default: gauss_bwd_mc<0>(a, s); break;
+    }
+    return hipGetLastError();
+}
+
+template <int MC>
+static void gauss_bwd_multi_mc(const MultiArgs &a, hipStream_t s) {
+    k_gauss_bwd_multi<MC><<<div_up(a.P, kShBlock), kShBlock, multi_lds_bytes<MC>(), s>>>(a);
+}
+
+hipError_t launch_gauss_bwd_multi(const MultiArgs &a, hipStream_t s) {
+    if (a.P == 0 || a.nv == 0) return hipSuccess;
+    switch (a.shs ? a.M : 0) {  // the caller checked M in {1, 4, 9, 16} when shs are given
+        case 16: gauss_bwd_multi_mc<16>(a, s); break;
+        case 9: gauss_bwd_multi_mc<9>(a, s); break;
+        case 4: gauss_bwd_multi_mc<4>(a, s); break;
+        case 1: gauss_bwd_multi_mc<1>(a, s); break;
+        default: gauss_bwd_multi_mc<0>(a, s); break;
     }
     return hipGetLastError();
 }

@@ -66,6 +66,29 @@ hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 
+// Per-Gaussian backward over several views of the same Gaussians (gsr_backward_gaussians): one
+// launch reads the parameters and read-modify-writes every gradient once for up to kMultiViews views.
+constexpr int kMultiViews = 8;
+struct MultiView {
+    const float *viewmatrix, *projmatrix, *campos;
+    CamStrides cs;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    const int *radii;
+    const uint32_t *goff;   // the view's emission offsets (GEOM)
+    const float4 *rec;      // the view's render records (GEOM): the activated opacity (sigmoid chain)
+    const float4 *part;     // the view's per-pair records (SCRATCH, gsr_backward_render)
+    float *dL_dmeans2D;     // the view's screen-space gradient (P,3) or NULL
+    int acc2;               // add into dL_dmeans2D instead of overwriting
+};
+struct MultiArgs {
+    int P, D, M, nv, act, accm;
+    float scale_modifier;
+    const float *means3D, *scales, *rotations, *shs, *cov3D_precomp;
+    float *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales, *dL_drot;
+    MultiView v[kMultiViews];
+};
+hipError_t launch_gauss_bwd_multi(const MultiArgs &a, hipStream_t s);
+
 // fused L1 + SSIM (gsr_loss.hip): normalised 1-D window of calc_ssim (external.py:48-65)
 struct SsimWindow { float w[11]; };
 size_t ssim_partials(int planes, int H, int W);

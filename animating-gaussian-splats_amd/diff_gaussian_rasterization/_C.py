@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "gsr_ssim_scratch_bytes", "gsr_l1_ssim_forward", "gsr_l1_ssim_backward",
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
-    "gsr_grad_fence",
+    "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians",
 )
 
 
@@ -60,6 +60,12 @@ class _Grads(ctypes.Structure):
         "dL_dscales", "dL_drotations")] + [("accumulate", ctypes.c_int)]
 
 
+class _ViewGrad(ctypes.Structure):  # gsr_view_grad (ABI 12)
+    _fields_ = [("cam", ctypes.POINTER(_Camera)), ("radii", ctypes.c_void_p), ("geom", ctypes.c_void_p),
+                ("scratch", ctypes.c_void_p), ("num_rendered", ctypes.c_int),
+                ("dL_dmeans2D", ctypes.c_void_p), ("accumulate_means2D", ctypes.c_int)]
+
+
 _ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
 _lib = None
 
@@ -81,6 +87,12 @@ def load_library():
     L.gsr_backward.restype = i
     L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
                                vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]
+    L.gsr_backward_render.restype = i
+    L.gsr_backward_render.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
+                                      vp, _ALLOC_FN, vp, vp]
+    L.gsr_backward_gaussians.restype = i
+    L.gsr_backward_gaussians.argtypes = [i, ctypes.POINTER(_ViewGrad), ctypes.POINTER(_Gaussians),
+                                         ctypes.POINTER(_Grads), vp]
     L.gsr_grad_fence.restype = i
     L.gsr_grad_fence.argtypes = [ctypes.POINTER(vp), i, vp]
     L.gsr_mark_visible.restype = i
@@ -116,7 +128,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 11  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 12  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -257,6 +269,42 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return nr.value, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
 
 
+def _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused, accumulate_into,
+                  skip=()):
+    """The 8 gradient outputs of the backward (output order) and the accumulate bits: a given
+    ``accumulate_into`` tensor is used in place, every other output is allocated (``skip``: output
+    slots not produced at all, returned as None)."""
+    e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731 - every element is written
+    has = lambda t: t is not None and t.numel() > 0  # noqa: E731
+    keep_col = not skip_unused or has(colors)
+    keep_cov = not skip_unused or has(cov3D_precomp)
+    keep_sr = not skip_unused or (has(scales) and has(rotations))
+    shapes = [(P, 3), (P, 3) if keep_col else (0,), (P, 1), (P, 3), (P, 6) if keep_cov else (0,),
+              (P, M, 3), (P, 3) if keep_sr else (0,), (P, 4) if keep_sr else (0,)]
+    acc = list(accumulate_into or ()) + [None] * 8
+    out = []
+    acc_bits = 0
+    for k, shp in enumerate(shapes):  # outputs that accumulate into a caller tensor are not allocated
+        t = acc[k]
+        if k in skip:
+            out.append(None)
+            continue
+        if t is None or shp == (0,):
+            out.append(e(*shp))
+            continue
+        if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
+            raise RuntimeError(f"accumulate_into[{k}]: expected a contiguous float32 {shp} tensor on {dev}")
+        out.append(t)
+        acc_bits |= 1 << k
+    out = tuple(out)
+    if acc_bits:  # the kernel writes caller tensors on this stream: the allocator must not recycle
+        cs = torch.cuda.current_stream(dev)  # them before it is done (views on several streams)
+        for k in range(8):
+            if acc_bits >> k & 1:
+                out[k].record_stream(cs)
+    return out, acc_bits
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations,
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
@@ -275,31 +323,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device
-    e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731 - every element is written
-    has = lambda t: t is not None and t.numel() > 0  # noqa: E731
-    keep_col = not skip_unused or has(colors)
-    keep_cov = not skip_unused or has(cov3D_precomp)
-    keep_sr = not skip_unused or (has(scales) and has(rotations))
-    shapes = [(P, 3), (P, 3) if keep_col else (0,), (P, 1), (P, 3), (P, 6) if keep_cov else (0,),
-              (P, M, 3), (P, 3) if keep_sr else (0,), (P, 4) if keep_sr else (0,)]
-    acc = list(accumulate_into or ()) + [None] * 8
-    out = []
-    acc_bits = 0
-    for k, shp in enumerate(shapes):  # outputs that accumulate into a caller tensor are not allocated
-        t = acc[k]
-        if t is None or shp == (0,):
-            out.append(e(*shp))
-            continue
-        if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
-            raise RuntimeError(f"accumulate_into[{k}]: expected a contiguous float32 {shp} tensor on {dev}")
-        out.append(t)
-        acc_bits |= 1 << k
-    out = tuple(out)
-    if acc_bits:  # the kernel writes caller tensors on this stream: the allocator must not recycle
-        cs = torch.cuda.current_stream(dev)  # them before it is done (views on several streams)
-        for k in range(8):
-            if acc_bits >> k & 1:
-                out[k].record_stream(cs)
+    out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
+                                  accumulate_into)
     if P == 0:
         return out
     dpix = dL_dout_color.contiguous().float()
@@ -310,6 +335,75 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
         _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
                               geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
                               dpix.data_ptr(), None, alloc.cb, None, ctypes.byref(grads), _stream_ptr(dev)))
+    return out
+
+
+def rasterize_gaussians_backward_render(background, means3D, radii, colors, scales, rotations,
+                                        scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
+                                        tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
+                                        binningBuffer, imageBuffer, activations=0):
+    """The per-pixel half of ``rasterize_gaussians_backward`` (gsr_backward_render): returns the
+    view's SCRATCH byte buffer holding its per-(tile, Gaussian) gradient records, for
+    ``rasterize_gaussians_backward_views``."""
+    L = load_library()
+    keep = []
+    g, P, _ = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
+                         rotations, scale_modifier, cov3D_precomp, keep, activations)
+    H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
+    cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
+    dev = means3D.device
+    if P == 0:
+        return torch.empty(1, dtype=torch.uint8, device=dev)
+    dpix = dL_dout_color.contiguous().float()
+    keep.append(dpix)
+    alloc = _Allocator(dev)
+    with _device_guard(dev):
+        _check(L.gsr_backward_render(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
+                                     geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+                                     dpix.data_ptr(), alloc.cb, None, _stream_ptr(dev)))
+    return alloc.buffers[GSR_BUF_SCRATCH]
+
+
+def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations, scale_modifier,
+                                       cov3D_precomp, sh, degree, activations=0, skip_unused=True,
+                                       accumulate_into=None):
+    """The per-Gaussian half over several views of the same Gaussians (gsr_backward_gaussians), on the
+    current stream: returns the 8 gradients of ``rasterize_gaussians_backward`` summed over the views
+    (slot 0, dL/dmeans2D, is None: each view's goes to its own array).  ``views``: dicts with the
+    view's ``viewmatrix``, ``projmatrix``, ``tanfovx``, ``tanfovy``, ``image_height``, ``image_width``,
+    ``campos``, ``bg``, its ``radii``, ``geomBuffer``, ``scratch`` (from
+    ``rasterize_gaussians_backward_render``) and ``num_rendered``, and optionally ``means2D_grad``, a
+    contiguous (P, 3) fp32 tensor receiving its screen-space gradient (added into when
+    ``accumulate_means2D``).  The caller orders the views' render halves before this call."""
+    L = load_library()
+    keep = []
+    dev = means3D.device
+    g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=dev), scales, rotations,
+                         scale_modifier, cov3D_precomp, keep, activations)
+    out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
+                                  accumulate_into, skip=(0,))
+    if P == 0 or not views:
+        return out
+    cams = []
+    vg = (_ViewGrad * len(views))()
+    cs = torch.cuda.current_stream(dev)
+    for k, v in enumerate(views):
+        cam = _camera(v["viewmatrix"], v["projmatrix"], v["tanfovx"], v["tanfovy"], v["image_height"],
+                      v["image_width"], v["campos"], v["bg"], False, keep)
+        cams.append(cam)
+        m2 = v.get("means2D_grad")
+        if m2 is not None:
+            if tuple(m2.shape) != (P, 3) or m2.dtype != torch.float32 or not m2.is_contiguous() or m2.device != dev:
+                raise RuntimeError(f"views[{k}]['means2D_grad']: expected a contiguous float32 ({P}, 3) tensor on {dev}")
+            m2.record_stream(cs)
+        for t in (v["radii"], v["geomBuffer"], v["scratch"]):  # read on this stream, maybe allocated
+            t.record_stream(cs)                                 # on the view's
+        vg[k] = _ViewGrad(ctypes.pointer(cam), v["radii"].data_ptr(), v["geomBuffer"].data_ptr(),
+                          v["scratch"].data_ptr(), int(v["num_rendered"]),
+                          m2.data_ptr() if m2 is not None else None, int(bool(v.get("accumulate_means2D"))))
+    grads = _Grads(*[t.data_ptr() if t is not None and t.numel() else None for t in out], acc_bits)
+    with _device_guard(dev):
+        _check(L.gsr_backward_gaussians(len(views), vg, ctypes.byref(g), ctypes.byref(grads), _stream_ptr(dev)))
     return out
 
 

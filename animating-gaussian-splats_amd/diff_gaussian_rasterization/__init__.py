@@ -12,6 +12,8 @@ work runs in hand-written HIP kernels for gfx950 behind the C ABI of ``include/g
 """
 from __future__ import annotations
 
+import os
+import threading
 from typing import NamedTuple
 
 import torch
@@ -21,7 +23,7 @@ from torch.autograd.graph import get_gradient_edge
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_parameters"]
+           "rasterize_parameters", "set_deferred_backward"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -69,24 +71,123 @@ def _input_nodes(ctx, inputs):
     return [nf[pos[i]][0] if i in pos and pos[i] < len(nf) else None for i in inputs]
 
 
-def _accumulation_target(t, node=None):
+def _accumulation_target(t, node=None, create=False):
     """The leaf's existing ``.grad`` when the backward kernel may add into it in place (and the
     Function then returns None for it): a leaf requiring grad whose gradient is a contiguous fp32
     tensor of its shape, with no hooks that autograd's accumulation would have run, in a backward
     pass that will accumulate into that leaf (``_engine_accumulates``) without building a graph of
     the gradient (``create_graph``).  Gives the same value as autograd's AccumulateGrad (one fp32
     add, ``grad += new``) without its separate read-read-write pass; every other case returns the
-    gradient to autograd as stock Functions do."""
+    gradient to autograd as stock Functions do.  ``create``: a leaf that qualifies but has no
+    ``.grad`` yet gets a zero one (0 + g is what AccumulateGrad would have stored)."""
     if t is None or not isinstance(t, torch.Tensor) or t.numel() == 0 or not t.is_leaf or not t.requires_grad:
         return None
     g = t.grad
-    if g is None or g.dtype != torch.float32 or not g.is_contiguous() or g.shape != t.shape or g.requires_grad:
+    if g is None and not (create and t.dtype == torch.float32 and t.is_contiguous()):
+        return None
+    if g is not None and (g.dtype != torch.float32 or not g.is_contiguous() or g.shape != t.shape or g.requires_grad):
         return None
     if t._backward_hooks or getattr(t, "_post_accumulate_grad_hooks", None):
         return None
     if torch.is_grad_enabled() or not _engine_accumulates(t, node):
         return None
+    if g is None:
+        t.grad = g = torch.zeros_like(t)
     return g
+
+
+# ---- deferred multi-view per-Gaussian backward ------------------------------------------------
+# train.py:753-767 sums the losses of 5 views and runs ONE backward.  When every gradient a view's
+# backward produces lands in a leaf's .grad (the in-place accumulation above), the per-Gaussian half
+# of the backward can wait until the pass has run every view: each view's backward node runs only
+# the per-pixel half (gsr_backward_render) and queues its records; a callback at the end of the
+# backward pass (the engine's final callbacks, which run on the caller's current streams after the
+# leaf streams are synchronised) runs ONE per-Gaussian pass over all the queued views of the same
+# Gaussians (gsr_backward_gaussians), reading the parameters and read-modify-writing every gradient
+# array once instead of once per view.  .grad holds the summed result when backward() returns, as
+# with stock autograd; the fp32 additions are grouped differently (views summed first).
+_defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0"}
+_pending_lock = threading.Lock()
+_pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
+_queued = set()  # graph tasks whose flush callback is queued
+
+
+def set_deferred_backward(on: bool) -> bool:
+    """Enable / disable the deferred multi-view per-Gaussian backward; returns the previous setting."""
+    prev = _defer["on"]
+    _defer["on"] = bool(on)
+    return prev
+
+
+def _flush_pending():
+    """Final callback of a backward pass: one per-Gaussian pass per group of queued views.  Groups
+    of older passes that never flushed (a pass that raised) are dropped."""
+    task = torch._C._current_graph_task_id()
+    with _pending_lock:
+        groups = [g for (t, _), g in _pending.items() if t == task]
+        for k in [k for k in _pending if k[0] <= task]:
+            del _pending[k]
+        _queued.discard(task)
+    for grp in groups:
+        dev = grp["device"]
+        with torch.cuda.device(dev):
+            cur = torch.cuda.current_stream(dev)
+            for s in grp["streams"]:  # every view's render half precedes the per-Gaussian pass
+                if s != cur:
+                    cur.wait_stream(s)
+            (means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act) = grp["gauss"]
+            _C.rasterize_gaussians_backward_views(grp["views"], means3D, colors, scales, rotations,
+                                                  scale_modifier, cov3D, sh, degree, activations=act,
+                                                  skip_unused=True, accumulate_into=grp["targets"])
+
+
+def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn):
+    """Queue this view for the end-of-pass per-Gaussian backward when every gradient it must produce
+    can go into a leaf's .grad; returns True when queued (the Function then returns None for all).
+    ``render_fn()`` runs the view's per-pixel half and returns its SCRATCH buffer."""
+    if not _defer["on"]:
+        return False
+    means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act = gauss
+    P = means3D.shape[0]
+    if P == 0 or not means3D.is_cuda or (sh.numel() and sh.shape[1] not in (1, 4, 9, 16)):
+        return False
+    task = torch._C._current_graph_task_id()
+    if task < 0:
+        return False
+    op = ctx.leaves[2]
+    if need[leaf_inputs[2]] and (op is None or tuple(op.shape) != (P, 1)):
+        return False
+    targets = [None] * 8
+    for k, (t, i, node) in enumerate(zip(ctx.leaves, leaf_inputs, nodes)):
+        if i is None or not need[i]:
+            continue
+        tgt = _accumulation_target(t, node, create=True)
+        if tgt is None:
+            return False  # autograd must receive this gradient: immediate path
+        targets[k] = tgt
+    rs = ctx.raster_settings
+    scratch = render_fn()
+    ptr = lambda t: t.data_ptr() if t is not None and t.numel() else 0  # noqa: E731
+    key = (means3D.device, P, ptr(means3D), ptr(scales), ptr(rotations), ptr(cov3D), ptr(sh), ptr(colors),
+           int(degree), float(scale_modifier), int(act)) + tuple(ptr(t) for t in targets[1:])
+    view = {"viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix, "tanfovx": rs.tanfovx,
+            "tanfovy": rs.tanfovy, "image_height": rs.image_height, "image_width": rs.image_width,
+            "campos": rs.campos, "bg": rs.bg, "radii": radii, "geomBuffer": geomBuffer, "scratch": scratch,
+            "num_rendered": ctx.num_rendered, "means2D_grad": targets[0], "accumulate_means2D": True}
+    stream = torch.cuda.current_stream(means3D.device)
+    with _pending_lock:
+        grp = _pending.get((task, key))
+        if grp is None:
+            grp = _pending[(task, key)] = {"device": means3D.device, "views": [], "gauss": gauss,
+                                           "targets": targets, "streams": []}
+        grp["views"].append(view)
+        if stream not in grp["streams"]:
+            grp["streams"].append(stream)
+        queue = task not in _queued
+        _queued.add(task)
+    if queue:
+        torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
+    return True
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
@@ -128,8 +229,14 @@ class _RasterizeGaussians(torch.autograd.Function):
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                 sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
         inputs = (1, 3, 4, 0, 7, 2, 5, 6)  # input index of each leaf (grad output order)
+        nodes = _input_nodes(ctx, inputs)
+        gauss = (means3D, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
+                 rs.sh_degree, 0)
+        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad,
+                      lambda: _C.rasterize_gaussians_backward_render(*args)):
+            return (None,) * 9  # every gradient is added into its leaf's .grad at the end of the pass
         acc = [_accumulation_target(t, node) if ctx.needs_input_grad[i] else None
-               for t, i, node in zip(ctx.leaves, inputs, _input_nodes(ctx, inputs))]
+               for t, i, node in zip(ctx.leaves, inputs, nodes)]
         g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc))
         for k, t in enumerate(acc):
             if t is not None:
@@ -230,6 +337,14 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         inputs = (1, 3, 4, 0, None, 2, 5, 6)  # input index of each leaf (grad output order; no cov3D)
         nodes = _input_nodes(ctx, [i for i in inputs if i is not None])
         nodes.insert(4, None)
+        gauss = (means, colors, log_scales, quaternions, rs.scale_modifier, empty, sh, rs.sh_degree, _C.ACT_ALL)
+        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, need,
+                      lambda: _C.rasterize_gaussians_backward_render(
+                          rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
+                          rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,
+                          rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
+                          activations=_C.ACT_ALL)):
+            return (None,) * 8
         acc = [_accumulation_target(t, node) if i is not None and need[i] else None
                for t, i, node in zip(ctx.leaves, inputs, nodes)]
         if acc[2] is not None and acc[2].shape != (means.shape[0], 1):

@@ -472,6 +472,11 @@ def main():
                     help="HIP streams the step's views alternate over: one view's memory-bound "
                          "per-Gaussian backward overlaps the next view's VALU-bound render kernels; "
                          "libgsr orders the gradient writes across streams (bitwise the 1-stream result)")
+    ap.add_argument("--step-shape", default="summed", choices=["summed", "per-view"],
+                    help="summed (train.py:753-767): the step's view losses summed, ONE backward -- each "
+                         "view's per-pixel backward runs in its node and one per-Gaussian pass covers all "
+                         "views at the end of the pass (deferred multi-view backward); per-view: a "
+                         "backward per view")
     ap.add_argument("--submit", default="serial", choices=["threads", "serial"],
                     help="threads: one host thread per stream submits that stream's views, so a forward "
                          "waiting for its num_rendered read-back blocks only its own thread and the other "
@@ -594,7 +599,14 @@ def main():
         # forwards run during the all-reduce and only its first gradient write waits for it.
         vs = views_of(it)
         ns = len(streams)
-        if pool is not None:  # view k on stream k % ns, submitted by that stream's thread
+        if args.step_shape == "summed":  # forwards on the streams, then one backward of the summed loss
+            imgs = []
+            for k, ci in enumerate(vs):
+                with torch.cuda.stream(streams[k % ns]):
+                    imgs.append(GaussianRasterizer(raster_settings=cams[ci])(**leaves)[0])
+            torch.autograd.backward(imgs, [dl] * len(imgs))
+            del imgs
+        elif pool is not None:  # view k on stream k % ns, submitted by that stream's thread
             futs = [pool.submit(run_views, vs[k::ns], streams[k]) for k in range(min(ns, len(vs)))]
             for f in futs:
                 f.result()
@@ -785,6 +797,8 @@ def main():
                        "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
                        "mean_num_rendered": int(K), "max_tile_pairs": max_tile, "parallelism": f"camera-dp{world}" if args.config != "C5"
                        else f"frame-dp{world}", "streams_per_gpu": len(streams),
+                       "step_shape": ("view losses summed, one backward (deferred multi-view per-Gaussian "
+                                      "pass)" if args.step_shape == "summed" else "one backward per view"),
                        "submission": "one host thread per stream" if pool is not None else "one host thread",
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
@@ -825,7 +839,7 @@ class _C5Fit:
     as train.py runs it (train.py:738-776: render 5 views, L1 + SSIM losses, backward, Adam step):
     5 rig views through rasterize_parameters (fused activations), the fused L1 + SSIM loss against the
     frame's target images (renders of the frame's ground-truth cloud, made before timing: the
-    captured images of a real sequence are resident too), backward per view on the HIP streams, one
+    captured images of a real sequence are resident too), the view losses summed and one backward, one
     FusedAdam step (densify.py:68-86 learning rates)."""
 
     def __init__(self, cfg, params_cpu, cams, rank, world, V, dev, streams, main_stream, total_steps):
@@ -874,15 +888,17 @@ class _C5Fit:
         f = self.frames[it % len(self.frames)]
         for s in self.streams:
             s.wait_stream(self.main)  # the previous iteration's Adam update
+        losses = []
         for k, ci in enumerate(self.frame_views(f)):
             with torch.cuda.stream(self.streams[k % len(self.streams)]):
                 img = self.rasterize(self.params, self.cams[ci])[0]
                 tgt = self.targets.get((f, ci))
                 if tgt is None:
                     raise RuntimeError(f"C5: no target for frame {f} view {ci}")
-                splat_loss.image_loss(img, tgt).backward()
+                losses.append(splat_loss.image_loss(img, tgt))
         for s in self.streams:
             self.main.wait_stream(s)
+        sum(losses).backward()  # train.py:757-767: the views' losses summed, one backward
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
 

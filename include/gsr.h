@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 11
+#define GSR_ABI_VERSION 12
 
 enum gsr_status {
     GSR_OK = 0,
@@ -144,6 +144,40 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
                  const void *geom, const void *binning, const void *image, const float *dL_dcolor,
                  const float *dL_ddepth, gsr_alloc_fn alloc, void *alloc_ctx, gsr_grads *out,
                  void *stream);
+
+/* ---- Multi-view backward (ABI >= 12) ------------------------------------------------------------
+ * gsr_backward split in two so that the per-Gaussian half runs ONCE for all the views of a step
+ * (train.py:753-767 sums the losses of 5 views before one backward):
+ *
+ *   gsr_backward_render     the per-pixel half of gsr_backward for one view: requests its SCRATCH
+ *                           buffer through `alloc` and fills it with the view's per-(tile, Gaussian)
+ *                           gradient records.  Keep SCRATCH (and the view's GEOM, radii) alive until
+ *                           gsr_backward_gaussians has been queued.
+ *   gsr_backward_gaussians  the per-Gaussian half over `nviews` such views of the SAME Gaussians `g`:
+ *                           every per-Gaussian gradient of `out` receives the SUM over the views
+ *                           (added into the arrays marked in out->accumulate, as gsr_backward does);
+ *                           each view's dL/dmeans2D goes to that view's own array.  out->dL_dmeans2D
+ *                           is ignored.  All views' gsr_backward_render work must be complete on
+ *                           `stream` or ordered before it by the caller (same stream or events).
+ *
+ * The result equals gsr_backward per view with the gradients summed, up to the order of the fp32
+ * additions (views are summed in registers, then added to the arrays once).  SH needs M in
+ * {1, 4, 9, 16} (GSR_ERR_UNSUPPORTED otherwise). */
+typedef struct gsr_view_grad {
+    const gsr_camera *cam;   /* the view's camera (as given to its gsr_forward) */
+    const int *radii;        /* the view's radii (P) */
+    const void *geom;        /* the view's GEOM buffer */
+    const void *scratch;     /* the view's SCRATCH buffer, filled by gsr_backward_render */
+    int num_rendered;        /* the view's num_rendered */
+    float *dL_dmeans2D;      /* (P,3) the view's screen-space gradient, or NULL */
+    int accumulate_means2D;  /* nonzero: add into dL_dmeans2D instead of overwriting it */
+} gsr_view_grad;
+
+int gsr_backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
+                        const void *geom, const void *binning, const void *image, const float *dL_dcolor,
+                        gsr_alloc_fn alloc, void *alloc_ctx, void *stream);
+int gsr_backward_gaussians(int nviews, const gsr_view_grad *views, const gsr_gaussians *g, gsr_grads *out,
+                           void *stream);
 
 /* Cross-stream order of gradient writes (ABI >= 10).  gsr_backward calls that write the same
  * gradient array (any of the gsr_grads pointers, accumulated or not) from different streams are
