@@ -524,11 +524,9 @@ __device__ inline void cov3d_backward(float3 s3, float mod, float4 q, const floa
 template <int MC> constexpr int kRecChunk = 3 * 256 * 16 <= 64 * sh_row_stride(MC) * 4 ? 256 : 128;
 template <int MC> constexpr int kRecStageF4 = 3 * kRecChunk<MC>;  // float4 per wave slice
 template <int C>  // records per staged chunk (the wave's LDS slice holds 3 C float4)
-__device__ inline void sum_records_chunked(int i, int P, const uint32_t *__restrict__ goff,
-                                           const float4 *__restrict__ part, float4 *stage,
-                                           float (&acc)[kPartial]) {
+__device__ inline void sum_records_span(uint32_t e0, uint32_t e1, const float4 *__restrict__ part,
+                                        float4 *stage, float (&acc)[kPartial]) {
     const int lane = threadIdx.x & 63;
-    const uint32_t e0 = goff[min(i, P)], e1 = goff[min(i + 1, P)];  // both in flight at once
     const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0);
     const uint32_t E1 = __builtin_amdgcn_readlane(e1, 63);
 #pragma unroll
@@ -554,6 +552,13 @@ __device__ inline void sum_records_chunked(int i, int P, const uint32_t *__restr
         }
         wave_lds_sync();
     }
+}
+template <int C>
+__device__ inline void sum_records_chunked(int i, int P, const uint32_t *__restrict__ goff,
+                                           const float4 *__restrict__ part, float4 *stage,
+                                           float (&acc)[kPartial]) {
+    const uint32_t e0 = goff[min(i, P)], e1 = goff[min(i + 1, P)];  // both in flight at once
+    sum_records_span<C>(e0, e1, part, stage, acc);
 }
 template <int MC>
 __device__ inline void sum_records_wave(int i, int P, const uint32_t *__restrict__ goff,
@@ -819,7 +824,18 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
 // read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
-constexpr int kMultiChunk = 128;  // records per staged chunk (6 KB of LDS per wave)
+#ifndef GSR_MV_CHUNK
+#define GSR_MV_CHUNK 128
+#endif
+constexpr int kMultiChunk = GSR_MV_CHUNK;  // records per staged chunk (48 B each, per wave)
+#ifndef GSR_MV_WPE
+#define GSR_MV_WPE 0  // waves per SIMD the register budget is held to (0: the compiler's choice)
+#endif
+#if GSR_MV_WPE
+#define GSR_MV_ATTR __attribute__((amdgpu_waves_per_eu(GSR_MV_WPE, 8)))
+#else
+#define GSR_MV_ATTR
+#endif
 template <int MC>
 constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_stride(MC) + 3) & ~size_t(3)) : 0; }
 template <int MC>
@@ -828,7 +844,7 @@ constexpr size_t multi_lds_bytes() {
 }
 
 template <int MC>  // SH coefficient count (1, 4, 9, 16), or 0 without SH (colours precomputed)
-__global__ __launch_bounds__(kShBlock) void k_gauss_bwd_multi(const MultiArgs a) {
+__global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const MultiArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     float4 *stage = reinterpret_cast<float4 *>(s_sh + multi_sh_floats<MC>()) + (threadIdx.x >> 6) * (3 * kMultiChunk);
@@ -866,12 +882,23 @@ __global__ __launch_bounds__(kShBlock) void k_gauss_bwd_multi(const MultiArgs a)
     bool vis = false;
     float o_act = 0.f;  // the activated opacity, from the record of a view that sees the Gaussian
     const int active = (a.D + 1) * (a.D + 1);
+    // each view's emission span and radius are loaded one view ahead (their latency then hides
+    // behind the previous view's records and chains instead of opening every view)
+    const int ic = min(i, P);
+    uint32_t e0n = a.v[0].goff[ic], e1n = a.v[0].goff[min(i + 1, P)];
+    int rn = a.v[0].radii[ii];
     for (int v = 0; v < a.nv; ++v) {
         const MultiView &V = a.v[v];
+        const uint32_t e0 = e0n, e1 = e1n;
+        const int rv = rn;
+        if (v + 1 < a.nv) {
+            const MultiView &Vn = a.v[v + 1];
+            e0n = Vn.goff[ic]; e1n = Vn.goff[min(i + 1, P)]; rn = Vn.radii[ii];
+        }
         float acc[kPartial];
-        sum_records_chunked<kMultiChunk>(i, P, V.goff, V.part, stage, acc);  // wave-collective
+        sum_records_span<kMultiChunk>(e0, e1, V.part, stage, acc);  // wave-collective
         if (!live) continue;
-        const bool r = V.radii[i] > 0;
+        const bool r = rv > 0;
         if (V.dL_dmeans2D) {
             float o2[3];
             old_load(V.dL_dmeans2D, 3 * (size_t)i, V.acc2, o2);

@@ -477,8 +477,9 @@ def main():
                          "view's per-pixel backward runs in its node and one per-Gaussian pass covers all "
                          "views at the end of the pass (deferred multi-view backward); per-view: a "
                          "backward per view")
-    ap.add_argument("--submit", default="serial", choices=["threads", "serial"],
-                    help="threads: one host thread per stream submits that stream's views, so a forward "
+    ap.add_argument("--submit", default="auto", choices=["auto", "threads", "serial"],
+                    help="auto: threads for the summed step (+4 %% measured: tools/ab_submit.sh), serial "
+                         "for per-view; threads: one host thread per stream submits that stream's views, so a forward "
                          "waiting for its num_rendered read-back blocks only its own thread and the other "
                          "streams' views keep the GPU fed; serial: one thread submits every view in turn")
     ap.add_argument("--backend", default="nccl",
@@ -581,9 +582,16 @@ def main():
         _C.grad_fence(*grads_of())
 
     pool = None
+    if args.submit == "auto":
+        args.submit = "threads" if args.step_shape == "summed" else "serial"
     if args.submit == "threads" and len(streams) > 1:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(max_workers=len(streams))
+
+    def forward_views(vs, s):  # one stream's share of a summed step's forwards
+        torch.cuda.set_device(dev)
+        with torch.cuda.stream(s):
+            return [GaussianRasterizer(raster_settings=cams[ci])(**leaves)[0] for ci in vs]
 
     def run_views(vs, s):  # one stream's share of a step, fwd + bwd per view
         torch.cuda.set_device(dev)
@@ -600,10 +608,13 @@ def main():
         vs = views_of(it)
         ns = len(streams)
         if args.step_shape == "summed":  # forwards on the streams, then one backward of the summed loss
-            imgs = []
-            for k, ci in enumerate(vs):
-                with torch.cuda.stream(streams[k % ns]):
-                    imgs.append(GaussianRasterizer(raster_settings=cams[ci])(**leaves)[0])
+            if pool is not None:  # stream k's views submitted by its own host thread
+                futs = [pool.submit(forward_views, vs[k::ns], streams[k]) for k in range(min(ns, len(vs)))]
+                imgs = [img for f in futs for img in f.result()]
+            else:
+                imgs = []
+                for k, ci in enumerate(vs):
+                    imgs += forward_views([ci], streams[k % ns])
             torch.autograd.backward(imgs, [dl] * len(imgs))
             del imgs
         elif pool is not None:  # view k on stream k % ns, submitted by that stream's thread

@@ -8,24 +8,25 @@
 # outputs: gpurun_out/prof_<tag>/{trace,fetch,write,sq1,sq2}/ raw CSV, trace_summary.txt, hbm_pmc.json, sq_pmc.json
 set -u
 tag=${1:-r01}; shift || true
+BENCH_LEGS="--call-site-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0"
 R=$(pwd)
 O=$R/gpurun_out/prof_$tag
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -- \
-    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
+    python3 "$R/bench.py" --no-cpu-baseline $BENCH_LEGS "$@" > "$O/trace.log" 2>&1 || { echo "trace pass failed rc=$?"; exit 1; }
 echo "trace ok"
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/fetch" -- \
-    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 2; }
+    python3 "$R/bench.py" --no-cpu-baseline $BENCH_LEGS "$@" > "$O/fetch.log" 2>&1 || { echo "fetch pass failed rc=$?"; exit 2; }
 echo "fetch ok"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/write" -- \
-    python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 3; }
+    python3 "$R/bench.py" --no-cpu-baseline $BENCH_LEGS "$@" > "$O/write.log" 2>&1 || { echo "write pass failed rc=$?"; exit 3; }
 echo "write ok"
 for pass in 1 2; do
   if [ $pass = 1 ]; then CTR="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE";
   else CTR="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_WAIT_ANY SQ_INSTS_VALU_TRANS_F32"; fi
   timeout -k 10 400 rocprofv3 --pmc $CTR --kernel-include-regex "render|gauss_bwd|preprocess|bin_emit" --kernel-trace --output-format csv -d "$O/sq$pass" -- \
-      python3 "$R/bench.py" --no-cpu-baseline "$@" > "$O/sq$pass.log" 2>&1 || { echo "sq pass $pass failed rc=$?"; exit 4; }
+      python3 "$R/bench.py" --no-cpu-baseline $BENCH_LEGS "$@" > "$O/sq$pass.log" 2>&1 || { echo "sq pass $pass failed rc=$?"; exit 4; }
 done
 echo "sq ok"
 cd "$R"

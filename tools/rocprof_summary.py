@@ -25,6 +25,10 @@ import sys
 from collections import defaultdict
 
 
+PER_STEP = {"k_gauss_bwd_multi"}  # kernels launched once per bench step (summed step shape)
+VIEWS = 5                         # views per step (bench.py --views-per-rank)
+
+
 def _short(name):
     m = re.search(r"gsr::(\w+?)(?:<|\(|$)", name) or re.search(r"(k_\w+)", name)
     return m.group(1) if m else name.split("(")[0][:60]
@@ -49,7 +53,12 @@ def trace(d, last=0, rng=None):
     if rng:  # launches [a, b) of each once-per-view kernel: bench.py's timed region
         a, b = rng
         for k, v in acc.items():
-            if len(v) >= b:
+            if k in PER_STEP:  # once per step (the multi-view per-Gaussian pass): [a/V, b/V)
+                a2, b2 = a // VIEWS, b // VIEWS
+                if len(v) >= b2:
+                    out[k]["timed_avg_us"] = sum(v[a2:b2]) / (b2 - a2)
+                    out[k]["timed_launches"] = [a2, b2]
+            elif len(v) >= b:
                 out[k]["timed_avg_us"] = sum(v[a:b]) / (b - a)
                 out[k]["timed_launches"] = [a, b]
     return dict(sorted(out.items(), key=lambda kv: -kv[1]["total_us"]))
