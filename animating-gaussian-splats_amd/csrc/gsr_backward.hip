@@ -102,6 +102,9 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 #ifndef GSR_BWD_ANY
 #define GSR_BWD_ANY 1  // skip the wave reduction of pairs no pixel of the wave took (0: always reduce)
 #endif
+#ifndef GSR_BWD_QM_REG
+#define GSR_BWD_QM_REG 0  // 1: the quarter mask by v_readlane from the staging lane (measured 1.5 % slower)
+#endif
 #ifndef GSR_BWD_WAVES
 #define GSR_BWD_WAVES 4  // items (one wave each) per workgroup
 #endif
@@ -288,7 +291,10 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             const float4 a = s_a[j], b = s_b[j], c = s_c[j];
 #endif
             const uint32_t p = (uint32_t)(start + j);
-            const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));  // wave-uniform quarter mask
+            // wave-uniform quarter mask, read from the staging lane's register (not the LDS copy), so
+            // the scalar branches below need not wait for the LDS reads
+            const uint32_t qm = GSR_BWD_QM_REG ? __builtin_amdgcn_readlane(qmask, j)
+                                               : __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));
             const PairX x = pair_x(a, pfx);
             // per-lane sums over this lane's pixels: S0 = sum G dL/dalpha, S1 = sum G dL/dalpha dy,
             // S4 = sum G dL/dalpha dy^2, cs = sum alpha T dL/dpix (the lane's 4 pixels share dx)
