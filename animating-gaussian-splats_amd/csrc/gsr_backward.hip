@@ -830,10 +830,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
 // read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
-#ifndef GSR_MV_CHUNK
-#define GSR_MV_CHUNK 128
-#endif
-constexpr int kMultiChunk = GSR_MV_CHUNK;  // records per staged chunk (48 B each, per wave)
+constexpr int kMultiChunk = 128;  // records per staged chunk (48 B each, per wave): 6 KB of LDS
 #ifndef GSR_MV_WPE
 #define GSR_MV_WPE 0  // waves per SIMD the register budget is held to (0: the compiler's choice)
 #endif
@@ -847,6 +844,20 @@ constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_str
 template <int MC>
 constexpr size_t multi_lds_bytes() {
     return sizeof(float) * multi_sh_floats<MC>() + sizeof(float4) * 3 * kMultiChunk * (kShBlock / 64);
+}
+
+// The lane's share of one record chunk [cb, min(cb + 128, E1)): six float4 held in named registers
+// (an array live across the view loop's control flow stays in scratch memory).  Clamped index:
+// every load in bounds, none predicated.
+struct RecChunk { float4 b0, b1, b2, b3, b4, b5; };
+__device__ inline RecChunk mv_load(const float4 *__restrict__ part, uint32_t cb, uint32_t E1, int lane) {
+    const uint32_t n3 = 3u * min(128u, E1 - cb);
+    const float4 *src = part + 3 * (size_t)cb;
+    RecChunk c;
+    c.b0 = src[min(lane + 0u, n3 - 1u)];   c.b1 = src[min(lane + 64u, n3 - 1u)];
+    c.b2 = src[min(lane + 128u, n3 - 1u)]; c.b3 = src[min(lane + 192u, n3 - 1u)];
+    c.b4 = src[min(lane + 256u, n3 - 1u)]; c.b5 = src[min(lane + 320u, n3 - 1u)];
+    return c;
 }
 
 template <int MC>  // SH coefficient count (1, 4, 9, 16), or 0 without SH (colours precomputed)
@@ -893,6 +904,14 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     const int ic = min(i, P);
     uint32_t e0n = a.v[0].goff[ic], e1n = a.v[0].goff[min(i + 1, P)];
     int rn = a.v[0].radii[ii];
+    // The records of all views stream through the wave's LDS slice in chunks of kMultiChunk, the
+    // loads of the next chunk -- of this view, or the next view's first -- in flight while the
+    // current chunk is summed and while a finished view's chains run (buf: 3 kMultiChunk / 64 float4
+    // per lane).  Same additions in the same order as sum_records_span.
+    static_assert(kMultiChunk == 128, "RecChunk holds 128 records");
+    const int lane = threadIdx.x & 63;
+    RecChunk buf = {};
+    bool have = false;  // buf holds (or is loading) the chunk the walk consumes next
     for (int v = 0; v < a.nv; ++v) {
         const MultiView &V = a.v[v];
         const uint32_t e0 = e0n, e1 = e1n;
@@ -902,7 +921,34 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             e0n = Vn.goff[ic]; e1n = Vn.goff[min(i + 1, P)]; rn = Vn.radii[ii];
         }
         float acc[kPartial];
-        sum_records_span<kMultiChunk>(e0, e1, V.part, stage, acc);  // wave-collective
+#pragma unroll
+        for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
+        const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0), E1 = __builtin_amdgcn_readlane(e1, 63);
+        if (E0 < E1 && !have) buf = mv_load(V.part, E0, E1, lane);
+        for (uint32_t cb = E0; cb < E1; cb += kMultiChunk) {  // wave-collective
+            stage[lane] = buf.b0; stage[lane + 64] = buf.b1; stage[lane + 128] = buf.b2;
+            stage[lane + 192] = buf.b3; stage[lane + 256] = buf.b4; stage[lane + 320] = buf.b5;
+            have = false;
+            if (cb + kMultiChunk < E1) {
+                buf = mv_load(V.part, cb + kMultiChunk, E1, lane);
+                have = true;
+            } else if (v + 1 < a.nv) {
+                const uint32_t E0n = __builtin_amdgcn_readfirstlane(e0n), E1n = __builtin_amdgcn_readlane(e1n, 63);
+                if (E0n < E1n) {
+                    buf = mv_load(a.v[v + 1].part, E0n, E1n, lane);
+                    have = true;
+                }
+            }
+            wave_lds_sync();
+            const uint32_t lo = max(e0, cb), hi = min(e1, cb + kMultiChunk);
+            for (uint32_t e = lo; e < hi; ++e) {
+                const float4 pa = stage[3 * (e - cb)], pb = stage[3 * (e - cb) + 1];
+                const float pc = reinterpret_cast<const float *>(stage + 3 * (e - cb) + 2)[0];
+                acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
+                acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc;
+            }
+            wave_lds_sync();
+        }
         if (!live) continue;
         const bool r = rv > 0;
         if (V.dL_dmeans2D) {
