@@ -24,6 +24,10 @@
 
 using namespace gsr;
 
+#ifndef GSR_FWD_ITEMS
+#define GSR_FWD_ITEMS 1  // 0: the backward builds its item list even when the forward could (A/B)
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -243,6 +247,9 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 size_t gsr_geom_bytes(int P) { return GeomLayout(P < 0 ? 0 : P).total; }
 size_t gsr_image_bytes(int W, int H, int P) { return ImageLayout(W, H, P < 0 ? 0 : P).total; }
 size_t gsr_binning_bytes(int K) { return BinningLayout(K).total; }
+size_t gsr_backward_items_bytes(int K, int W, int H) {
+    return bwd_items_bytes(K < 0 ? 0 : K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH));
+}
 size_t gsr_scratch_bytes(int K, int W, int H) {
     return ScratchLayout(K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH)).total;
 }
@@ -319,14 +326,20 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     const uint32_t n_mid = __atomic_load_n(hw.h + 1, __ATOMIC_ACQUIRE);
     const uint32_t n_vlong = __atomic_load_n(hw.h + 2, __ATOMIC_ACQUIRE);
     const uint32_t max_n = __atomic_load_n(hw.h + 3, __ATOMIC_ACQUIRE);
+    // BINNING = the binning arrays, [the backward's item list], [the long-list merge buffer]
     const size_t bin_bytes = BinningLayout((int)K).total;
+    const size_t item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)K, a.gx * a.gy) : 0;
     const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
-    char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, bin_bytes + tmp_bytes);
+    char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, bin_bytes + item_bytes + tmp_bytes);
     if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
     carve_binning(a, bin, (int)K);
     { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, (int)K, s)); }
-    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)(bin + bin_bytes), s)); }
+    { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)(bin + bin_bytes + item_bytes), s)); }
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
+    if (GSR_FWD_ITEMS && g->prepare_backward) {  // the backward's item list, built here, off its critical path
+        Phase ph(s, "bwd_items");
+        HIP_TRY(launch_bwd_items_raw((int)K, a.gx * a.gy, a.ranges, a.tile_maxc, (uint2 *)(bin + bin_bytes), s));
+    }
     return GSR_OK;
 }
 
@@ -364,9 +377,14 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, SL.total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
     a.part = (float4 *)(scr + SL.part);
-    a.items = (uint2 *)(scr + SL.items);
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
-    { Phase ph(s, "bwd_items"); HIP_TRY(launch_bwd_items(a, s)); }
+    if (GSR_FWD_ITEMS && g->prepare_backward) {  // built by the forward, after the binning arrays
+        a.items = (uint2 *)((char *)binning + BinningLayout(num_rendered).total);
+    } else {
+        a.items = (uint2 *)(scr + SL.items);
+        Phase ph(s, "bwd_items");
+        HIP_TRY(launch_bwd_items(a, s));
+    }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
     return GSR_OK;
 }

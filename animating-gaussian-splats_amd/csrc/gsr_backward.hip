@@ -1068,10 +1068,14 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 
 
 // ==========================================================================================
-hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
-    if (a.K == 0) return hipSuccess;
-    k_bwd_items<<<1, 1024, 0, s>>>(a.gx * a.gy, a.ranges, a.tile_maxc, a.items);
+hipError_t launch_bwd_items_raw(int K, int T, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
+                                hipStream_t s) {
+    if (K == 0) return hipSuccess;
+    k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items);
     return hipGetLastError();
+}
+hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
+    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.ranges, a.tile_maxc, a.items, s);
 }
 
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {

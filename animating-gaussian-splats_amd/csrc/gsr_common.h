@@ -161,6 +161,11 @@ struct BinningLayout {
     }
 };
 
+// The backward's work-item list ([0].x = count, then (tile, segment) in dispatch order): in SCRATCH,
+// or -- when the forward prepares the backward (gsr_gaussians.prepare_backward) -- right after the
+// BINNING arrays (at BinningLayout(K).total), built by the forward.
+__host__ __device__ inline size_t bwd_items_bytes(int K, int T) { return align256(sizeof(uint2) * (max_bwd_items(K, T) + 1)); }
+
 // SCRATCH (backward): one 48-byte partial-gradient record per Gaussian-tile pair, stored at the
 // pair's EMISSION index (Gaussian-major), so each Gaussian's records are contiguous for the
 // per-Gaussian reduction: (dmean2D.xy, dconic.a, dconic.b) (dconic.c, dopacity, dcolour.rg)
@@ -172,7 +177,7 @@ struct ScratchLayout {
         const size_t k = size_t(K > 0 ? K : 1);
         size_t o = 0;
         part = o;  o = align256(o + sizeof(float4) * 3 * k);
-        items = o; o = align256(o + sizeof(uint2) * (max_bwd_items(K, T) + 1));
+        items = o; o += bwd_items_bytes(K, T);
         total = o;
     }
 };

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "gsr_ssim_scratch_bytes", "gsr_l1_ssim_forward", "gsr_l1_ssim_backward",
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
-    "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians",
+    "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
 )
 
 
@@ -51,7 +51,7 @@ class _Gaussians(ctypes.Structure):
                 ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
                 ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
                 ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
-                ("activations", ctypes.c_int)]
+                ("activations", ctypes.c_int), ("prepare_backward", ctypes.c_int)]
 
 
 class _Grads(ctypes.Structure):
@@ -100,8 +100,9 @@ def load_library():
     for n in ("gsr_geom_bytes", "gsr_binning_bytes"):
         getattr(L, n).restype = ctypes.c_size_t
         getattr(L, n).argtypes = [i]
-    L.gsr_scratch_bytes.restype = ctypes.c_size_t
-    L.gsr_scratch_bytes.argtypes = [i, i, i]
+    for n in ("gsr_scratch_bytes", "gsr_backward_items_bytes"):
+        getattr(L, n).restype = ctypes.c_size_t
+        getattr(L, n).argtypes = [i, i, i]
     L.gsr_image_bytes.restype = ctypes.c_size_t
     L.gsr_image_bytes.argtypes = [i, i, i]
     L.gsr_last_error.restype = ctypes.c_char_p
@@ -230,7 +231,7 @@ def _mat16(m):
 
 
 def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier, cov3D, keep,
-               activations=0):
+               activations=0, prepare_backward=False):
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     P = means3D.size(0)
@@ -240,18 +241,21 @@ def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_mo
     M = sh.size(1) if sh is not None and sh.numel() else 0
     return _Gaussians(P, int(degree), M, float(scale_modifier), _ptr(means3D), _ptr(sh), _ptr(colors),
                       _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(cov3D),
-                      int(activations)), P, M
+                      int(activations), int(bool(prepare_backward))), P, M
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
-                        image_width, sh, degree, campos, prefiltered, debug=False, activations=0):
+                        image_width, sh, degree, campos, prefiltered, debug=False, activations=0,
+                        prepare_backward=False):
     """``activations`` (ACT_* bits): opacity / scales / rotations hold the raw parameters of
-    shared.py:29-42 and are activated inside the kernels (0 = the reference's interface)."""
+    shared.py:29-42 and are activated inside the kernels (0 = the reference's interface).
+    ``prepare_backward``: a backward will follow; the forward also builds its work-item list (the
+    backward calls must then pass the same flag)."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
-                         cov3D_precomp, keep, activations)
+                         cov3D_precomp, keep, activations, prepare_backward)
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, campos,
                   background, prefiltered, keep)
     dev = means3D.device
@@ -309,7 +313,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
-                                 activations=0, skip_unused=False, accumulate_into=None):
+                                 activations=0, skip_unused=False, accumulate_into=None,
+                                 prepare_backward=False):
     """Returns the 8 gradients of the upstream binding.  ``skip_unused``: gradients of inputs that
     were not given (colours under SH, cov3D under scales/rotations and vice versa) come back as
     empty tensors and their HBM writes are skipped.  ``accumulate_into``: optional sequence of 8
@@ -319,7 +324,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
-                         rotations, scale_modifier, cov3D_precomp, keep, activations)
+                         rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward)
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device
@@ -341,14 +346,14 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 def rasterize_gaussians_backward_render(background, means3D, radii, colors, scales, rotations,
                                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                         tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
-                                        binningBuffer, imageBuffer, activations=0):
+                                        binningBuffer, imageBuffer, activations=0, prepare_backward=False):
     """The per-pixel half of ``rasterize_gaussians_backward`` (gsr_backward_render): returns the
     view's SCRATCH byte buffer holding its per-(tile, Gaussian) gradient records, for
     ``rasterize_gaussians_backward_views``."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
-                         rotations, scale_modifier, cov3D_precomp, keep, activations)
+                         rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward)
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device

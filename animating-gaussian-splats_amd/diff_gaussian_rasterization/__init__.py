@@ -193,19 +193,22 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales,
-                                     rotations, cov3Ds_precomp, raster_settings)
+                                     rotations, cov3Ds_precomp, raster_settings, torch.is_grad_enabled())
 
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                cov3Ds_precomp, raster_settings):
+                cov3Ds_precomp, raster_settings, grad_mode=False):
         rs = raster_settings
         args = (rs.bg, means3D, colors_precomp, opacities, scales, rotations, rs.scale_modifier,
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
                 rs.image_height, rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered)
+        # a backward can follow (grad mode at the call, an input requiring grad): the forward
+        # prepares it
+        ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = \
-            _C.rasterize_gaussians(*args)
+            _C.rasterize_gaussians(*args, prepare_backward=ctx.prep)
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
@@ -221,30 +224,31 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, grad_depth):
         if grad_out_color is None:  # only depth was used: it carries no gradient (-w-depth)
-            return (None,) * 9
+            return (None,) * 10
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
          binningBuffer, imgBuffer) = ctx.saved_tensors
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                 sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
+        kw = {"prepare_backward": ctx.prep}
         inputs = (1, 3, 4, 0, 7, 2, 5, 6)  # input index of each leaf (grad output order)
         nodes = _input_nodes(ctx, inputs)
         gauss = (means3D, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
                  rs.sh_degree, 0)
         if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad,
-                      lambda: _C.rasterize_gaussians_backward_render(*args)):
-            return (None,) * 9  # every gradient is added into its leaf's .grad at the end of the pass
+                      lambda: _C.rasterize_gaussians_backward_render(*args, **kw)):
+            return (None,) * 10  # every gradient is added into its leaf's .grad at the end of the pass
         acc = [_accumulation_target(t, node) if ctx.needs_input_grad[i] else None
                for t, i, node in zip(ctx.leaves, inputs, nodes)]
-        g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc))
+        g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc, **kw))
         for k, t in enumerate(acc):
             if t is not None:
                 g[k] = None  # already accumulated into the leaf's .grad
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp,
          grad_sh, grad_scales, grad_rotations) = g
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities,
-                grad_scales, grad_rotations, grad_cov3Ds_precomp, None)
+                grad_scales, grad_rotations, grad_cov3Ds_precomp, None, None)
 
 
 class GaussianRasterizer(nn.Module):
@@ -302,18 +306,21 @@ def rasterize_parameters(params, raster_settings, means2D=None, shs=None):
         shs = torch.empty(0, device=means.device)
     return _RasterizeGaussianParameters.apply(means, means2D, shs, colors, params["opacity_logits"],
                                               params["log_scales"], params["rotation_quaternions"],
-                                              raster_settings)
+                                              raster_settings, torch.is_grad_enabled())
 
 
 class _RasterizeGaussianParameters(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, means, means2D, sh, colors, opacity_logits, log_scales, quaternions, raster_settings):
+    def forward(ctx, means, means2D, sh, colors, opacity_logits, log_scales, quaternions, raster_settings,
+                grad_mode=False):
         rs = raster_settings
         empty = torch.empty(0, device=means.device)
+        ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)  # a backward can follow
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians(
             rs.bg, means, colors, opacity_logits, log_scales, quaternions, rs.scale_modifier, empty,
             rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
-            rs.sh_degree, rs.campos, rs.prefiltered, activations=_C.ACT_ALL)
+            rs.sh_degree, rs.campos, rs.prefiltered, activations=_C.ACT_ALL,
+            prepare_backward=ctx.prep)
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.opacity_shape = opacity_logits.shape
@@ -328,7 +335,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, _grad_depth):
         if grad_out_color is None:
-            return (None,) * 8
+            return (None,) * 9
         rs = ctx.raster_settings
         colors, means, log_scales, quaternions, radii, sh, geomBuffer, binningBuffer, imgBuffer = \
             ctx.saved_tensors
@@ -343,8 +350,8 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                           rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                           rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,
                           rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                          activations=_C.ACT_ALL)):
-            return (None,) * 8
+                          activations=_C.ACT_ALL, prepare_backward=ctx.prep)):
+            return (None,) * 9
         acc = [_accumulation_target(t, node) if i is not None and need[i] else None
                for t, i, node in zip(ctx.leaves, inputs, nodes)]
         if acc[2] is not None and acc[2].shape != (means.shape[0], 1):
@@ -354,10 +361,10 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                 rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
                 rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc)
+                activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc, prepare_backward=ctx.prep)
         done = [t is not None for t in acc]  # accumulated into the leaf's .grad: return None
         return (None if done[3] else g_means, None if (done[0] or not need[1]) else g_means2D,
                 None if (done[5] or not sh.numel()) else g_sh,
                 None if (done[1] or not colors.numel()) else g_colors,
                 None if done[2] else g_opacity.view(ctx.opacity_shape),
-                None if done[6] else g_scales, None if done[7] else g_rot, None)
+                None if done[6] else g_scales, None if done[7] else g_rot, None, None)

@@ -600,15 +600,16 @@ def main():
                 img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
                 img.backward(dl)
 
-    def step(it):
+    def step(it, solo=False):
         # No stream waits for another at the step start: libgsr orders the gradient writes across
         # streams, record_stream keeps freed gradients from early reuse, and for N > 1 the bucket's
         # all-reduce + reset on the main stream is declared with grad_fence, so the next step's
         # forwards run during the all-reduce and only its first gradient write waits for it.
+        # solo: one stream, one submitting thread (per-kernel times without concurrency)
         vs = views_of(it)
-        ns = len(streams)
+        ns = 1 if solo else len(streams)
         if args.step_shape == "summed":  # forwards on the streams, then one backward of the summed loss
-            if pool is not None:  # stream k's views submitted by its own host thread
+            if pool is not None and not solo:  # stream k's views submitted by its own host thread
                 futs = [pool.submit(forward_views, vs[k::ns], streams[k]) for k in range(min(ns, len(vs)))]
                 imgs = [img for f in futs for img in f.result()]
             else:
@@ -679,6 +680,18 @@ def main():
     _C.profile_enable(False)
     probe = {ph: _C.profile_read(ph) for ph in PHASES}
     dom = max(PHASES, key=lambda ph: probe[ph][0])
+    # untimed solo probe (C3 / C3M / C4): the same steps on one stream, one thread -- each kernel's
+    # time without the other streams' kernels sharing the CUs (the roofline's kernel alone)
+    solo = None
+    if c5 is None and args.probe_steps > 0:
+        torch.cuda.synchronize()
+        _C.profile_reset()
+        _C.profile_enable(True)
+        for it in range(args.probe_steps):
+            step(args.warmup + it, solo=True)
+        torch.cuda.synchronize()
+        _C.profile_enable(False)
+        solo = {ph: _C.profile_read(ph) for ph in PHASES}
     # timed region: HIP events only around the dominant kernel (its roofline), host timers on
     if dist is not None:
         dist.barrier()
@@ -770,6 +783,9 @@ def main():
                 pk = 1024 * q["clock_ghz"] / 2  # Ginst/s at that clock
                 valu["profile_clock_ghz"] = round(q["clock_ghz"], 3)
                 valu["issue_frac_at_profile_clock"] = round(rate / pk, 4)
+    solo_ms = solo[dom][0] / solo[dom][1] if solo and solo[dom][1] else None
+    if valu is not None and solo_ms:
+        valu["solo_issue_frac"] = round(valu["insts_per_launch"] / (solo_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, SH)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
@@ -819,6 +835,9 @@ def main():
                          "traffic_2x_fetch": traffic_2x,
                          "traffic_calibration": "profiles/r01_fetch_calib.txt" if traffic else None,
                          "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch),
+                         # the same kernel alone (solo probe: one stream, no concurrent kernels)
+                         "solo_avg_kernel_ms": round(solo_ms, 5) if solo_ms else None,
+                         "solo_frac": round(bytes_launch / (solo_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5) if solo_ms else None,
                          "algorithmic_bytes_formula": {"render_bwd": "K*40 + N*20 + T*16",
                                                        "render_fwd": "K*44 + N*24 + T*16",
                                                        "gauss_bwd": "P*(84+F) + P*(56+F)"}.get(dom),
@@ -830,6 +849,8 @@ def main():
                                       "achieved_GBps_per_gpu": round(pipe_gbps, 1),
                                       "frac": round(pipe_gbps / HBM_PEAK_GBPS, 4)}},
             "phase_ms_per_launch": {ph: round(probe[ph][0] / max(probe[ph][1], 1), 5) for ph in PHASES},
+            "phase_ms_per_launch_solo": {ph: round(solo[ph][0] / max(solo[ph][1], 1), 5) for ph in PHASES}
+            if solo else None,
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
             "call_site": call_site,

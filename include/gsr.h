@@ -101,6 +101,11 @@ typedef struct gsr_gaussians {
     const float *rotations;      /* (P,4)   or NULL */
     const float *cov3D_precomp;  /* (P,6)   or NULL */
     int activations;             /* gsr_activation bit mask (ABI >= 2); 0 = activated inputs */
+    /* ABI >= 12.  gsr_forward: nonzero = a backward will follow, so the forward also builds the
+     * backward's work-item list (one small kernel after the blend, off the backward's critical path)
+     * in gsr_backward_items_bytes() extra bytes at the end of the BINNING buffer.  gsr_backward /
+     * gsr_backward_render: must equal the value the forward was called with. */
+    int prepare_backward;
 } gsr_gaussians;
 
 /* Bits of gsr_grads.accumulate (ABI >= 6), one per output array. */
@@ -197,6 +202,8 @@ size_t gsr_geom_bytes(int P);
 size_t gsr_image_bytes(int width, int height, int P);
 size_t gsr_binning_bytes(int num_rendered);
 size_t gsr_scratch_bytes(int num_rendered, int width, int height);
+/* Extra BINNING bytes gsr_forward requests when gsr_gaussians.prepare_backward is set (ABI 12). */
+size_t gsr_backward_items_bytes(int num_rendered, int width, int height);
 
 /* Introspection for parity tests: byte offsets of the arrays inside the three forward buffers, in
  * this order: geom {depth, rec (64-byte render records), rect, tiles, goff}, image {ranges,
