@@ -636,6 +636,9 @@ __global__ __launch_bounds__(512) void k_merge_pass(int T, const uint32_t *__res
 // render record and tests it against quarter q = pixel rows 4q..4q+3 with a conservative ellipse
 // bound), then wave q blends its 16x4 quarter (one pixel per lane) over the entries whose bit q is
 // set; saturated quarters skip their evaluations and the walk ends when all four are saturated.
+#ifndef GSR_FWD_Q8
+#define GSR_FWD_Q8 1  // 8x8 quarters per wave (0: 16x4 strips, the backward's quarters)
+#endif
 __global__ __launch_bounds__(256) void k_render_fwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
     const uint4 *__restrict__ pairs,
@@ -670,12 +673,28 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     }
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = tile % gx, ty = tile / gx;
-    const int px = tx * kTileW + (lane & 15);
-    const int py = ty * kTileH + 4 * wv + (lane >> 4);
+#if GSR_FWD_Q8
+    // wave q blends the 8x8 quarter (8 (q & 1), 8 (q >> 1)) of the tile: a compact footprint crosses
+    // fewer quarters than a 16x4 strip (tools/contrib_stats.py: 1.54 vs 1.73 evaluated quarters per
+    // list entry at C3)
+    const int lx = 8 * (wv & 1) + (lane & 7), ly = 8 * (wv >> 1) + (lane >> 3);
+#else
+    const int lx = lane & 15, ly = 4 * wv + (lane >> 4);  // 16x4 strips
+#endif
+    const int px = tx * kTileW + lx;
+    const int py = ty * kTileH + ly;
     const float pfx = (float)px, pfy = (float)py;
+    // this pixel's slot in the backward's layout (16x4 strip k = ly / 4, lane = 16 (ly % 4) + lx)
+    const int bslot = 64 * (ly >> 2) + 16 * (ly & 3) + lx;
     // staging role: thread 4e + q handles entry e of the batch against quarter q
     const int se = threadIdx.x >> 2, sq = threadIdx.x & 3;
+#if GSR_FWD_Q8
+    const float qx0 = (float)(tx * kTileW + 8 * (sq & 1)), qy0 = (float)(ty * kTileH + 8 * (sq >> 1));
+    constexpr int kQW = 8, kQH = 8;
+#else
     const float qx0 = (float)(tx * kTileW), qy0 = (float)(ty * kTileH + 4 * sq);
+    constexpr int kQW = kTileW, kQH = 4;
+#endif
     const bool inside = px < W && py < H;
     bool done = !inside;
     if (threadIdx.x == 0) s_live = 0;
@@ -709,9 +728,11 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         // segment boundary (kSeg entries): this quarter's blend state before entry `base`, the state a
         // backward segment's reverse walk starts from; stored while the quarter is live, i.e. for
         // every boundary below its pixels' last contributor (done pixels store their final state)
-        if (base > 0 && (base & (kSeg - 1)) == 0 && ((live >> wv) & 1u)) {
+        // (8x8 quarters: every quarter stores while any is live -- the backward reads whole 16x4 strips,
+        // which span two quarters; a finished pixel's state is its final one)
+        if (base > 0 && (base & (kSeg - 1)) == 0 && (GSR_FWD_Q8 || ((live >> wv) & 1u))) {
             const size_t b = (size_t)seg_off[tile] + (uint32_t)base / kSeg - 1u;
-            seg_state[b * kTilePix + 64 * wv + lane] = make_float4(C0, C1, C2, Tt);
+            seg_state[b * kTilePix + bslot] = make_float4(C0, C1, C2, Tt);
         }
         // ---- stage the batch (block-wide) ----
         bool hit = false;
@@ -721,7 +742,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             if (pv) {
                 if (sq < 3) s_u.st.rec[sq][se] = pr;
                 hit = ((live >> sq) & 1u) &&
-                      !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kTileW - 1), qy0 + 3);
+                      !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kQW - 1), qy0 + (kQH - 1));
             }
             GSR_FWD_FETCH(base + 64);
         }
@@ -732,7 +753,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1];
             if (sq < 3) s_u.st.rec[sq][se] = rec[(size_t)kRecF4 * g + sq];
             hit = ((live >> sq) & 1u) &&
-                  !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kTileW - 1), qy0 + 3);
+                  !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kQW - 1), qy0 + (kQH - 1));
         }
 #endif
         // combine the 4 quarter bits of entry se (lanes 4e..4e+3 of this wave) with DPP
@@ -775,10 +796,24 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         out_color[2 * H * W + pid] = C2 + Tt * bg[2];
         out_depth[pid] = Dp;
     }
+#if GSR_FWD_Q8
+    // per 16x4 strip maximum of n_contrib (the backward's quarters): rows 4k..4k+3 = half of the lanes of
+    // two waves; lanes (lane >> 3) < 4 hold strip 2 (wv >> 1), the others strip 2 (wv >> 1) + 1
+    uint32_t mx = last;
+#pragma unroll
+    for (int d = 16; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));  // within 32 lanes
+    __syncthreads();  // every wave is past its last read of s_u
+    if (threadIdx.x < 4) s_u.st.q[threadIdx.x] = 0;
+    __syncthreads();
+    if ((lane & 31) == 0) atomicMax(&s_u.st.q[2 * (wv >> 1) + (lane >> 5)], mx);
+    __syncthreads();
+    if (threadIdx.x < 4) tile_maxc[4 * tile + threadIdx.x] = s_u.st.q[threadIdx.x];
+#else
     uint32_t mx = last;
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
     if (lane == 0) tile_maxc[4 * tile + wv] = mx;
+#endif
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
 #endif
