@@ -105,7 +105,10 @@ def _accumulation_target(t, node=None, create=False):
 # leaf streams are synchronised) runs ONE per-Gaussian pass over all the queued views of the same
 # Gaussians (gsr_backward_gaussians), reading the parameters and read-modify-writing every gradient
 # array once instead of once per view.  .grad holds the summed result when backward() returns, as
-# with stock autograd; the fp32 additions are grouped differently (views summed first).
+# with stock autograd; the fp32 additions are grouped differently (views summed first).  Queued views
+# are keyed by the engine's graph-task id; a pass that raises never runs its callback, and the next
+# flush drops its views -- so backward passes through this path must not run concurrently from
+# several threads (set_deferred_backward(False) for that).
 _defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0"}
 _pending_lock = threading.Lock()
 _pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
