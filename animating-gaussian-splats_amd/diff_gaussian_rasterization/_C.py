@@ -156,20 +156,23 @@ def _f32(t):
 
 
 class _Allocator:
-    """ctypes allocation callback handing out torch byte tensors on the current device."""
+    """ctypes allocation callback handing out torch byte tensors on the current device.  The callback
+    closes over the buffer dict only -- a callback bound to the allocator itself would make a reference
+    cycle that keeps every workspace alive until Python's cyclic collector runs (GBs at C3)."""
 
     def __init__(self, device):
         self.device = device
-        self.buffers = {}
-        self.cb = _ALLOC_FN(self._alloc)
+        buffers = self.buffers = {}
 
-    def _alloc(self, _ctx, which, nbytes):
-        try:
-            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
-        except Exception:  # noqa: BLE001 - reported through the C ABI as GSR_ERR_ALLOC
-            return None
-        self.buffers[int(which)] = t
-        return t.data_ptr()
+        def alloc(_ctx, which, nbytes):
+            try:
+                t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+            except Exception:  # noqa: BLE001 - reported through the C ABI as GSR_ERR_ALLOC
+                return None
+            buffers[int(which)] = t
+            return t.data_ptr()
+
+        self.cb = _ALLOC_FN(alloc)
 
 
 class _device_guard:

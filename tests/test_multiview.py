@@ -208,3 +208,32 @@ def test_views_abi_matches_per_view_sum(cuda):
     for k in range(len(cams)):
         ref = per[k][0] + (5.0 if k == 1 else 0.0)
         assert torch.equal(m2[k], ref), k  # the screen-space gradient is the record sum itself: exact
+
+
+def test_workspaces_freed_without_the_cyclic_collector(cuda):
+    """Forward / backward workspaces (GEOM, BINNING, IMAGE, SCRATCH) are freed by reference counting
+    as soon as the graph and the queued views are released: with the cyclic collector off, device
+    memory returns to its starting level after every step (an allocator callback bound to its owner
+    once kept every workspace alive until a gc run)."""
+    import gc
+    a, deg = _inputs(cuda, "sh3")
+    cams = _cams(cuda, 3, deg)
+    dls = [S.upstream_grad(H, W, seed=120 + k, device=cuda) for k in range(len(cams))]
+    leaves = _leaves(a)
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    gc.disable()
+    try:
+        for deferred in (True, False):
+            prev = set_deferred_backward(deferred)
+            try:
+                for _ in range(3):
+                    _views_loss(leaves, cams, dls).backward()
+                    for v in leaves.values():
+                        v.grad = None
+                    torch.cuda.synchronize()
+                    assert torch.cuda.memory_allocated() == base, deferred
+            finally:
+                set_deferred_backward(prev)
+    finally:
+        gc.enable()
