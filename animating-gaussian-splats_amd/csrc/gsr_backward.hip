@@ -336,12 +336,12 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             if (!GSR_BWD_ANY || __ballot(any)) {
                 // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
                 const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
-                if ((lane & 15) < 2) {  // lanes 0 and 1 of each row hold the two halves of its sums:
-                    // both are added into the zeroed slot, 0 + h0 + h1 == h0 + h1 in either order
+                if ((lane & 15) < kRedLanes) {  // the first kRedLanes lanes of each row hold its partial
+                    // sums, added into the zeroed slot (2 lanes: 0 + h0 + h1 == h0 + h1 in either order)
                     float *o = s_out + j * kPartial;
                     lds_add(o + xslot, sm.X);
                     lds_add(o + yslot, sm.Y);
-                    if (lane < 2) lds_add(o + 5, sm.Z);
+                    if (lane < kRedLanes) lds_add(o + 5, sm.Z);
                 }
             }
         }

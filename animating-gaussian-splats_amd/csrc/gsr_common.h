@@ -725,6 +725,20 @@ __device__ inline float row_sum16_pairs(float v) {
 // a row hold them).  Row totals:
 //   X rows: [sum dx S0, sum S4, sum S1, sum cs0]    Y rows: [sum dx^2 S0, sum cs1, sum dx S1, sum cs2]
 //   Z row 0: sum S0
+// GSR_BWD_RED_STAGES: DPP stages of the row sums (3: lanes 0-1 of a row hold its halves; 2: lanes
+// 0-3 its quarters; 1: lanes 0-7 its eighths) -- the rest is added by LDS atomics into the slot
+#ifndef GSR_BWD_RED_STAGES
+#define GSR_BWD_RED_STAGES 3
+#endif
+constexpr int kRedLanes = 16 >> GSR_BWD_RED_STAGES;  // lanes per row that add their partial sum
+__device__ inline float row_sum16_part(float v) {
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
+    if (GSR_BWD_RED_STAGES >= 2)
+        v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
+    if (GSR_BWD_RED_STAGES >= 3)
+        v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+    return v;
+}
 struct PairSums { float X, Y, Z; };
 __device__ inline PairSums wave_pair_sums(float S0, float S1, float S4, float cs0, float cs1, float cs2,
                                           float dx, int row) {
@@ -734,9 +748,9 @@ __device__ inline PairSums wave_pair_sums(float S0, float S1, float S4, float cs
     const float wx = row == 0 ? dx : 1.f;
     const float wy = row == 0 ? dx * dx : (row == 2 ? dx : 0.f);
     PairSums r;
-    r.X = row_sum16_pairs(rA * wx);
-    r.Y = row_sum16_pairs(fmaf(rA, wy, rC));
-    r.Z = row_sum16_pairs(rA);
+    r.X = row_sum16_part(rA * wx);
+    r.Y = row_sum16_part(fmaf(rA, wy, rC));
+    r.Z = row_sum16_part(rA);
     return r;
 }
 
