@@ -72,10 +72,53 @@ def main():
         b8 = geom.reshape(maxc, 2, 8, 2, 8).transpose(0, 1, 3, 2, 4).reshape(maxc, 4, 64)
         lc8 = lc.reshape(2, 8, 2, 8).transpose(0, 2, 1, 3).reshape(4, 64).max(-1)
         tot["pq8_geom"] = tot.get("pq8_geom", 0) + int((b8.any(-1) & (pidx[:, :, 0] < lc8[None])).sum())
+        # 8x4 half-quarters (two per 8x8 quarter)
+        b84 = geom.reshape(maxc, 4, 4, 2, 8).transpose(0, 1, 3, 2, 4).reshape(maxc, 8, 32)
+        lc84 = lc.reshape(4, 4, 2, 8).transpose(0, 2, 1, 3).reshape(8, 32).max(-1)
+        tot["pq84_geom"] = tot.get("pq84_geom", 0) + int((b84.any(-1) & (pidx[:, :, 0] < lc84[None])).sum())
+        # backward split into two 16x8 halves walking their own lists in one wave: steps per 64-entry batch
+        # = max over the halves of the entries each half walks (vs entries the whole tile walks)
+        top = geom[:, :8, :].reshape(maxc, -1).any(-1) & (np.arange(maxc) < lc[:8].max())
+        bot = geom[:, 8:, :].reshape(maxc, -1).any(-1) & (np.arange(maxc) < lc[8:].max())
+        anyq = gq.any(1)
+        steps = 0
+        # 16x2 strips of each half (rows 2k, 2k+1): a lane's 4 pixels share a column
+        st = geom.reshape(maxc, 2, 4, 2, 16).any(-1).any(-1)  # (entry, half, strip)
+        lch = lc.reshape(2, 4, 2, 16).max(-1).max(-1)          # (half, strip) max n_contrib
+        st = st & (np.arange(maxc)[:, None, None] < lch[None])
+        ev = 0
+        for b0 in range(0, maxc, 64):
+            ia = [e for e in range(b0, min(b0 + 64, maxc)) if top[e]]
+            ib = [e for e in range(b0, min(b0 + 64, maxc)) if bot[e]]
+            steps += max(len(ia), len(ib))
+            for t in range(max(len(ia), len(ib))):
+                ma = st[ia[t], 0] if t < len(ia) else np.zeros(4, bool)
+                mb = st[ib[t], 1] if t < len(ib) else np.zeros(4, bool)
+                ev += int((ma | mb).sum())
+        tot["half_evals"] = tot.get("half_evals", 0) + ev
+        # forward: each 8x8 quarter's wave split into two 8x4 halves walking their own lists
+        fs = 0
+        h84 = b84.any(-1)  # (entry, 8 halves): index = 4-row block * 2 + 8-column block
+        for q in range(4):
+            qy, qx = q >> 1, q & 1
+            i0, i1 = (2 * qy) * 2 + qx, (2 * qy + 1) * 2 + qx
+            ha = h84[:, i0] & (np.arange(maxc) < lc84[i0])
+            hb = h84[:, i1] & (np.arange(maxc) < lc84[i1])
+            for b0 in range(0, maxc, 64):
+                fs += max(int(ha[b0:b0 + 64].sum()), int(hb[b0:b0 + 64].sum()))
+        tot["fwd_half_steps"] = tot.get("fwd_half_steps", 0) + fs
+        tot["half_steps"] = tot.get("half_steps", 0) + steps
+        tot["half_pairs"] = tot.get("half_pairs", 0) + int(top.sum() + bot.sum())
     print(tot)
-    print("quarters per entry: geom %.3f live %.3f; pairs walked geom %.3f live %.3f; live/geom (pair,quarter) %.3f; 8x8 blocks per entry %.3f"
+    print("split-wave backward: half-pair walks per entry %.3f, wave steps per entry %.3f (now %.3f), "
+          "strip evaluations per entry %.3f (now %.3f quarter evaluations)"
+          % (tot["half_pairs"] / tot["entries"], tot["half_steps"] / tot["entries"], tot["pairs_geom"] / tot["entries"],
+             tot["half_evals"] / tot["entries"], tot["pq_geom"] / tot["entries"]))
+    print("forward with 8x4 half-waves: wave steps per entry %.3f (8x8 quarters now %.3f)"
+          % (tot["fwd_half_steps"] / tot["entries"], tot["pq8_geom"] / tot["entries"]))
+    print("quarters per entry: geom %.3f live %.3f; pairs walked geom %.3f live %.3f; live/geom (pair,quarter) %.3f; 8x8 blocks per entry %.3f, 8x4 halves per entry %.3f"
           % (tot["pq_geom"] / tot["entries"], tot["pq_live"] / tot["entries"], tot["pairs_geom"] / tot["entries"],
-             tot["pairs_live"] / tot["entries"], tot["pq_live"] / max(tot["pq_geom"], 1), tot["pq8_geom"] / tot["entries"]))
+             tot["pairs_live"] / tot["entries"], tot["pq_live"] / max(tot["pq_geom"], 1), tot["pq8_geom"] / tot["entries"], tot["pq84_geom"] / tot["entries"]))
 
 
 if __name__ == "__main__":
