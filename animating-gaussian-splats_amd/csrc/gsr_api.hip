@@ -227,7 +227,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.sort_lists = (uint32_t *)(base + L.sort_lists);
     a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
     a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
-    a.meta = (uint32_t *)(base + L.meta);
+    a.meta = (uint32_t *)(base + L.meta); a.chunk_off = (uint32_t *)(base + L.chunk_off);
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K);

@@ -959,7 +959,8 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             gput_old(V.dL_dmeans2D, 3 * i + 2, 0.f, V.acc2, o2[2]);
         }
         if (!r) continue;
-        if (!vis) o_act = V.rec[(size_t)kRecF4 * i + 1].y;  // written by every view that sees it
+        // the activated opacity (sigmoid chain only): written by every view that sees the Gaussian
+        if (!vis && (a.act & GSR_ACT_SIGMOID_OPACITY)) o_act = V.rec[(size_t)kRecF4 * i + 1].y;
         vis = true;
         gop += acc[5]; gc0 += acc[6]; gc1 += acc[7]; gc2 += acc[8];
         float vm[16], pj[16];

@@ -58,6 +58,9 @@ struct GeomLayout {
 #define GSR_BIN_THREADS 1024
 #endif
 constexpr int kBinThreads = GSR_BIN_THREADS;  // threads per binning block (one chunk of CH Gaussians)
+// Tile histogram kept in LDS when T * 4 B fits in 64 KiB; larger tile grids (e.g. 4K frames)
+// count straight into global memory.
+constexpr int kMaxLdsTiles = 16384;
 struct BinGrid {
     int CH, NB;
     __host__ __device__ BinGrid(int P) {
@@ -120,7 +123,7 @@ __host__ __device__ inline size_t max_bwd_items(int K, int T) {
 //            segment boundaries (seg_bounds) -> index of its first saved boundary state.
 struct ImageLayout {
     size_t ranges, pix_end, n_contrib, tile_maxc, tile_order_f, seg_off, sort_lists,
-        tile_count, tile_cursor, block_sums, block_off, meta, total;
+        tile_count, tile_cursor, block_sums, block_off, meta, chunk_off, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -138,6 +141,8 @@ struct ImageLayout {
         block_sums = o;  o = align256(o + sizeof(uint32_t) * (NB + 1));
         block_off = o;   o = align256(o + sizeof(uint32_t) * (NB + 1));
         meta = o;        o = align256(o + sizeof(uint32_t) * 16);
+        // (chunk, tile) counts, then each chunk's slab offset inside the tile's range (LDS binning)
+        chunk_off = o;   o = align256(o + (T <= kMaxLdsTiles ? sizeof(uint32_t) * (size_t)NB * T : 0));
         total = o;
     }
 };

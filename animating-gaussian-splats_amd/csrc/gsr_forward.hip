@@ -2,9 +2,11 @@
 //
 // Pipeline (one HIP stream, one host sync for the pair count K, as the reference does):
 //   k_preprocess   1 thread / Gaussian: cull, Sigma3D, EWA Sigma2D, conic, radius, tile rect, SH->RGB
-//   k_bin_count    chunked over Gaussians: LDS tile histogram -> one global add per (chunk, tile)
+//   k_bin_count    chunked over Gaussians: LDS tile histogram -> the chunk's row of a (chunk, tile)
+//                  count matrix
+//   k_bin_colscan  column scan of that matrix: each chunk's slab offset inside every tile, tile totals
 //   k_bin_scan     1 block: exclusive scan of tile counts -> tile ranges; scan of chunk sums; K
-//   k_bin_emit     chunked: re-count in LDS, reserve a (chunk, tile) slab, scatter one 16-byte
+//   k_bin_emit     chunked: slab starts into LDS (range start + column offset), scatter one 16-byte
 //                  record per pair (64-bit key depth_bits << 32 | gaussian + emission index) into
 //                  its tile's range; exclusive emission offsets
 //   k_tile_sort    1 block / tile: sort the tile's keys by (depth bits, index) in LDS (bitonic),
@@ -126,14 +128,16 @@ __global__ __launch_bounds__(256) void k_preprocess(
 }
 
 // ------------------------------------------------------------------------------------------
-// Tile histogram per chunk of Gaussians.  USE_LDS: histogram in LDS (T <= kMaxLdsTiles), then one
-// global atomic per non-empty (chunk, tile) bin -- lanes of a wave add to 64 consecutive counters.
+// Tile histogram per chunk of Gaussians.  USE_LDS (T <= kMaxLdsTiles): histogram in LDS, stored as
+// the chunk's row of the (chunk, tile) count matrix (coalesced, no global atomics; k_bin_colscan
+// turns the columns into slab offsets and tile totals).  Otherwise global atomics into tile_count.
 template <bool USE_LDS>
 __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T, int gx,
                                                    const uint2 *__restrict__ rects,
                                                    const uint32_t *__restrict__ tiles,
                                                    uint32_t *__restrict__ tile_count,
-                                                   uint32_t *__restrict__ block_sums) {
+                                                   uint32_t *__restrict__ block_sums,
+                                                   uint32_t *__restrict__ chunk_off) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_red[16];
     const int b = blockIdx.x;
@@ -160,10 +164,49 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
     if (threadIdx.x == 0) block_sums[b] = tot;
     if (USE_LDS) {
         __syncthreads();
-        for (int t = threadIdx.x; t < T; t += blockDim.x) {
-            const uint32_t c = s_hist[t];
-            if (c) atomicAdd(&tile_count[t], c);
-        }
+        uint32_t *row = chunk_off + (size_t)b * T;
+        for (int t = threadIdx.x; t < T; t += blockDim.x) row[t] = s_hist[t];
+    }
+}
+
+// Column scan of the (chunk, tile) count matrix: chunk_off[b][t] <- the counts of tile t over the
+// chunks before b (chunk b's slab start inside the tile's range), tile_count[t] <- the tile's total.
+// 1024 threads = kColW tile columns x kColG groups of consecutive chunks; a thread holds its group's
+// (at most kColR) counts in registers between the two passes, so the matrix is read once.  Replaces
+// one device-scope atomic per non-empty (chunk, tile) bin in k_bin_count and a returning one in
+// k_bin_emit (~2 M each at C3) with 2 x NB x T x 4 bytes of coalesced traffic.
+constexpr int kColW = 32, kColG = 32, kColR = 16;
+static_assert(kColG * kColR >= 512, "BinGrid makes at most 512 chunks");
+__global__ __launch_bounds__(1024) void k_bin_colscan(int T, int NB, uint32_t *__restrict__ chunk_off,
+                                                      uint32_t *__restrict__ tile_count) {
+    __shared__ uint32_t s_part[kColG][kColW + 1];
+    const int col = threadIdx.x % kColW, grp = threadIdx.x / kColW;
+    const int t = blockIdx.x * kColW + col;
+    const int R = div_up(NB, kColG);
+    const int r0 = min(NB, grp * R), r1 = min(NB, r0 + R);
+    uint32_t *p = chunk_off + t;
+    uint32_t v[kColR];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kColR; ++k) {
+        v[k] = (t < T && r0 + k < r1) ? p[(size_t)(r0 + k) * T] : 0u;
+        sum += v[k];
+    }
+    s_part[grp][col] = sum;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kColG; ++k) {
+        const uint32_t c = s_part[k][col];
+        pre += k < grp ? c : 0u;
+        tot += c;
+    }
+    if (t >= T) return;
+    if (grp == 0) tile_count[t] = tot;
+#pragma unroll
+    for (int k = 0; k < kColR; ++k) {
+        if (r0 + k < r1) p[(size_t)(r0 + k) * T] = pre;
+        pre += v[k];
     }
 }
 
@@ -312,45 +355,18 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
                                                   const uint32_t *__restrict__ block_off,
                                                   uint32_t *__restrict__ tile_cursor,
                                                   uint32_t *__restrict__ goff,
-                                                  uint4 *__restrict__ pairs, uint32_t K) {
+                                                  uint4 *__restrict__ pairs, uint32_t K,
+                                                  const uint32_t *__restrict__ chunk_off) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
     __shared__ uint32_t s_red[16];
     const int b = blockIdx.x;
     const int g0 = b * CH, g1 = min(P, g0 + CH);
     GSR_EMIT_STAMP(0);
-    if (USE_LDS) {
-        for (int t = threadIdx.x; t < T; t += blockDim.x) s_cur[t] = 0;
-        __syncthreads();
-        for (int g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
-            if (tiles[g] == 0) continue;
-            const uint2 r = rects[g];
-            const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
-            for (int y = y0; y < y1; ++y)
-                for (int x = x0; x < x1; ++x) atomicAdd(&s_cur[y * gx + x], 1u);
-        }
+    if (USE_LDS) {  // this chunk's slab in every tile: the tile's range start + the column scan
+        const uint32_t *row = chunk_off + (size_t)b * T;
+        for (int t = threadIdx.x; t < T; t += blockDim.x) s_cur[t] = tile_cursor[t] + row[t];
         __syncthreads();
         GSR_EMIT_STAMP(1);
-        // reserve the slabs: every thread's (up to kReserveBatch) returning global atomics are issued
-        // before any result is consumed, so their device-scope round trips overlap instead of
-        // queueing one behind another
-        constexpr int kReserveBatch = 8;
-        for (int t0 = threadIdx.x; t0 < T; t0 += kReserveBatch * (int)blockDim.x) {
-            uint32_t c[kReserveBatch], r[kReserveBatch];
-#pragma unroll
-            for (int i = 0; i < kReserveBatch; ++i) {
-                const int t = t0 + i * (int)blockDim.x;
-                c[i] = t < T ? s_cur[t] : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < kReserveBatch; ++i)
-                r[i] = c[i] ? atomicAdd(&tile_cursor[t0 + i * (int)blockDim.x], c[i]) : 0u;
-#pragma unroll
-            for (int i = 0; i < kReserveBatch; ++i) {
-                const int t = t0 + i * (int)blockDim.x;
-                if (t < T) s_cur[t] = r[i];
-            }
-        }
-        __syncthreads();
         GSR_EMIT_STAMP(2);
     }
     // emission offsets (exclusive scan of tiles over Gaussian index) + key scatter
@@ -865,9 +881,11 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;  // (tile_count was zeroed by k_preprocess)
     if (T <= kMaxLdsTiles)
-        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
-    else
-        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums);
+    {
+        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, a.chunk_off);
+        k_bin_colscan<<<div_up(T, kColW), 1024, 0, s>>>(T, bg.NB, a.chunk_off, a.tile_count);
+    } else
+        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, nullptr);
     return hipGetLastError();
 }
 
@@ -884,9 +902,9 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K);
+        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off);
     else
-        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K);
+        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off);
     return hipGetLastError();
 }
 

@@ -5,10 +5,6 @@
 
 namespace gsr {
 
-// Tile histogram kept in LDS when T * 4 B fits in 64 KiB; larger tile grids (e.g. 4K frames)
-// count straight into global memory.
-constexpr int kMaxLdsTiles = 16384;
-
 struct FwdArgs {
     // inputs
     int P, D, M, W, H, gx, gy, act;
@@ -21,7 +17,7 @@ struct FwdArgs {
     // image
     uint2 *ranges; float4 *pix_end; uint32_t *n_contrib; uint32_t *tile_maxc;
     uint32_t *tile_order_f; uint32_t *seg_off; uint32_t *sort_lists; uint32_t *tile_count;
-    uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta;
+    uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta; uint32_t *chunk_off;
     // binning
     uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
