@@ -171,13 +171,16 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
 
 // Column scan of the (chunk, tile) count matrix: chunk_off[b][t] <- the counts of tile t over the
 // chunks before b (chunk b's slab start inside the tile's range), tile_count[t] <- the tile's total.
-// 1024 threads = kColW tile columns x kColG groups of consecutive chunks; a thread holds its group's
+// kColW tile columns x kColG groups of consecutive chunks per block; a thread holds its group's
 // (at most kColR) counts in registers between the two passes, so the matrix is read once.  Replaces
 // one device-scope atomic per non-empty (chunk, tile) bin in k_bin_count and a returning one in
 // k_bin_emit (~2 M each at C3) with 2 x NB x T x 4 bytes of coalesced traffic.
-constexpr int kColW = 32, kColG = 32, kColR = 16;
+#ifndef GSR_COLSCAN_W
+#define GSR_COLSCAN_W 32  // tile columns per k_bin_colscan block (32 x kColG threads)
+#endif
+constexpr int kColW = GSR_COLSCAN_W, kColG = 32, kColR = 16;
 static_assert(kColG * kColR >= 512, "BinGrid makes at most 512 chunks");
-__global__ __launch_bounds__(1024) void k_bin_colscan(int T, int NB, uint32_t *__restrict__ chunk_off,
+__global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(int T, int NB, uint32_t *__restrict__ chunk_off,
                                                       uint32_t *__restrict__ tile_count) {
     __shared__ uint32_t s_part[kColG][kColW + 1];
     const int col = threadIdx.x % kColW, grp = threadIdx.x / kColW;
@@ -781,12 +784,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         // ---- blend this wave's quarter ----
         uint64_t m = __ballot((s_u.st.q[lane] >> wv) & 1u);
         if (!((live >> wv) & 1u)) m = 0;
-        while (m) {
-            const int j = __builtin_ctzll(m);
-            m &= m - 1;
-            const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
-            const Blend e = blend_eval(a, b, pfx, pfy);
-            const bool ok = !done && blend_ok(e);
+        // one entry's blend into this pixel's state (front to back)
+        auto take = [&](const Blend &e, float4 b, float4 c, int j, bool valid) {
+            const bool ok = valid && !done && blend_ok(e);
             const float test_T = fmaf(-e.alpha, Tt, Tt);  // T (1 - alpha), one rounding
             // keep == !(test_T < 1e-4) (test_T is never NaN: T in (0, 1], alpha in [0, 0.99]); the
             // pixel finishes when it takes the entry but may not keep it: (done | ok) & ~use, one
@@ -800,6 +800,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             Dp = fmaf(b.z, w, Dp);
             Tt = use ? test_T : Tt;
             last = use ? (uint32_t)(base + j + 1) : last;
+        };
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
+            take(blend_eval(a, b, pfx, pfy), b, c, j, true);
         }
         if (((live >> wv) & 1u) && !__ballot(!done) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
@@ -883,7 +889,7 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     if (T <= kMaxLdsTiles)
     {
         k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, a.chunk_off);
-        k_bin_colscan<<<div_up(T, kColW), 1024, 0, s>>>(T, bg.NB, a.chunk_off, a.tile_count);
+        k_bin_colscan<<<div_up(T, kColW), kColW * kColG, 0, s>>>(T, bg.NB, a.chunk_off, a.tile_count);
     } else
         k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, nullptr);
     return hipGetLastError();

@@ -468,6 +468,9 @@ def main():
     ap.add_argument("--views-per-rank", type=int, default=5,
                     help="C3 / C5: views rendered per GPU per step (train.py:753 optimises on the summed "
                          "losses of 5 views per step)")
+    ap.add_argument("--stream-priority", type=int, default=0,
+                    help="HIP priority of the view streams (negative = higher than the main stream, "
+                         "which runs the multi-view per-Gaussian pass and the collectives)")
     ap.add_argument("--streams", type=int, default=3,
                     help="HIP streams the step's views alternate over: one view's memory-bound "
                          "per-Gaussian backward overlaps the next view's VALU-bound render kernels; "
@@ -574,7 +577,7 @@ def main():
 
     main_stream = torch.cuda.current_stream(dev)
     # side streams for the views: the main stream keeps the collectives (N > 1) out of their way
-    streams = [torch.cuda.Stream(dev) for _ in range(max(args.streams, 1))]
+    streams = [torch.cuda.Stream(dev, priority=args.stream_priority) for _ in range(max(args.streams, 1))]
     for s in streams:
         s.wait_stream(main_stream)  # the setup's parameters, leaves and upstream gradient
 

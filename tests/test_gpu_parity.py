@@ -234,6 +234,20 @@ def test_long_tile_lists(P, cuda):
     check_backward(_gpu_backward(a, rs, cuda, fw, dl), O.backward(st, dl.numpy()), P, 0)
 
 
+def test_wide_frame_global_binning(cuda):
+    """A frame of more than kMaxLdsTiles = 16384 tiles (4224 x 1040: 264 x 65 = 17160 tiles) takes
+    the binning path that counts and reserves with global atomics instead of the LDS histogram +
+    (chunk, tile) column scan; its lists and ranges must be the same."""
+    W, H = 4224, 1040
+    a, rs = _inputs(30_000, W, H, 1100.0, 0.01, seed=8)
+    assert -(-W // 16) * -(-H // 16) > 16384
+    st = _ora_forward(a, rs)
+    fw = _gpu_forward(a, rs, cuda)
+    check_forward(fw, st)
+    dl = S.upstream_grad(H, W, device="cpu")
+    check_backward(_gpu_backward(a, rs, cuda, fw, dl), O.backward(st, dl.numpy()), 30_000, 0)
+
+
 def test_empty_and_all_culled(cuda):
     rs = S.render_settings(48, 32, S.intrinsics(48.0, 48, 32), S.look_at(0, 0, 4), device="cpu")
     rs = rs._replace(bg=torch.tensor([0.25, 0.5, 0.75]))
