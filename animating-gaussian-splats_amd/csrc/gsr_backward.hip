@@ -91,6 +91,17 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 // transmittance T and front colour C_f, so the colour behind, projected on dL/dpixel, is
 // AR = (<dL/dpix, C_all - C_f> + T_final <bg, dL/dpix>) / T -- otherwise the pixel's final state
 // (T_final, AR = <bg, dL/dpix>).
+// One 36-byte partial-gradient record at emission slot `em` of the packed record array: three
+// 12-byte stores (4-byte aligned), the kPartial values in slot order.
+struct __attribute__((packed, aligned(4))) F3 { float x, y, z; };
+__device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, float r2, float r3, float r4,
+                                 float r5, float r6, float r7, float r8) {
+    F3 *d = reinterpret_cast<F3 *>(reinterpret_cast<float *>(part) + (size_t)kRecF * em);
+    d[0] = F3{r0, r1, r2};
+    d[1] = F3{r3, r4, r5};
+    d[2] = F3{r6, r7, r8};
+}
+
 #ifndef GSR_BWD_WPE
 #define GSR_BWD_WPE 5  // waves per SIMD the register budget is held to (0: compiler's choice)
 #endif
@@ -151,10 +162,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     if (seg & kZeroItem) {  // zero records for one kZeroChunk of the slots past maxc (see bwd_zero_items)
         const int z0 = maxc + (int)kZeroChunk * (int)((seg & ~kZeroItem) + 1);
         for (int p = z0 + lane; p < min(n, z0 + (int)kZeroChunk); p += 64) {
-            float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
-            dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-            dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            dst[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rec_store(part, slot_emit[rg.x + p], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
         }
         return;
     }
@@ -162,10 +170,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     const int s1 = min(s1f, maxc);
     if (s1f >= maxc) {  // the tile's last segment item: the first kZeroChunk slots nobody reached
         for (int p = maxc + lane; p < min(n, maxc + (int)kZeroChunk); p += 64) {
-            float4 *dst = part + 3 * (size_t)slot_emit[rg.x + p];
-            dst[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-            dst[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            dst[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rec_store(part, slot_emit[rg.x + p], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f);
         }
     }
     const float half_w = (float)(0.5 * W), half_h = (float)(0.5 * H);
@@ -353,13 +358,13 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             for (int q = 0; q < kPartial; ++q) sm[q] = s2[q];
             const float o = s_b[lane].y;  // the moments of sG = opacity G dL/dalpha
             const float S1 = o * sm[0], S2 = o * sm[1];
-            float4 *dst = part + 3 * (size_t)em;
-            dst[0] = make_float4((-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
-                                 (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
-                                 -0.5f * (o * sm[2]),                 // dL/dconic.a
-                                 -0.5f * (o * sm[3]));                // dL/dconic.b (b/2 convention)
-            dst[1] = make_float4(-0.5f * (o * sm[4]), sm[5], sm[6], sm[7]);  // dconic.c, dopacity, dcolour.rg
-            dst[2] = make_float4(sm[8], 0.f, 0.f, 0.f);                // dcolour.b
+            rec_store(part, em,
+                      (-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
+                      (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
+                      -0.5f * (o * sm[2]),                 // dL/dconic.a
+                      -0.5f * (o * sm[3]),                 // dL/dconic.b (b/2 convention)
+                      -0.5f * (o * sm[4]),                 // dL/dconic.c
+                      sm[5], sm[6], sm[7], sm[8]);         // dL/dopacity, dL/dcolour
         }
     }
 #ifdef GSR_TRACE
@@ -529,6 +534,9 @@ __device__ inline void cov3d_backward(float3 s3, float mod, float4 q, const floa
 // kRecChunk: 256 records when the SH rows' LDS slice of a wave holds them (MC = 16), else 128.
 template <int MC> constexpr int kRecChunk = 3 * 256 * 16 <= 64 * sh_row_stride(MC) * 4 ? 256 : 128;
 template <int MC> constexpr int kRecStageF4 = 3 * kRecChunk<MC>;  // float4 per wave slice
+// A chunk of n packed records starting at record cb, as lane-contiguous float4 loads from the
+// 16-byte aligned address at or below its first float: (kRecF cb) & 3 floats of lead-in.
+__host__ __device__ constexpr int rec_chunk_f4(int C) { return (kRecF * C + 3 + 3) / 4; }
 template <int C>  // records per staged chunk (the wave's LDS slice holds 3 C float4)
 __device__ inline void sum_records_span(uint32_t e0, uint32_t e1, const float4 *__restrict__ part,
                                         float4 *stage, float (&acc)[kPartial]) {
@@ -537,24 +545,28 @@ __device__ inline void sum_records_span(uint32_t e0, uint32_t e1, const float4 *
     const uint32_t E1 = __builtin_amdgcn_readlane(e1, 63);
 #pragma unroll
     for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
-    constexpr int NF4 = 3 * C;
+    constexpr int NL = (rec_chunk_f4(C) + 63) / 64;  // float4 loads per lane
+    static_assert(64 * NL <= 3 * C, "the staged chunk fits the wave's LDS slice");
+    const float *pf = reinterpret_cast<const float *>(part);
     for (uint32_t cb = E0; cb < E1; cb += C) {
-        const uint32_t n3 = 3u * min((uint32_t)C, E1 - cb);
-        const float4 *src = part + 3 * (size_t)cb;
-        float4 v[NF4 / 64];
+        const size_t f0 = (size_t)kRecF * cb;
+        const uint32_t lead = (uint32_t)(f0 & 3u);
+        const uint32_t nf4 = (lead + kRecF * min((uint32_t)C, E1 - cb) + 3u) / 4u;
+        const float4 *src = reinterpret_cast<const float4 *>(pf + (f0 - lead));
+        float4 v[NL];
 #pragma unroll
-        for (int t = 0; t < NF4 / 64; ++t)  // clamped index: every load in bounds, none predicated
-            v[t] = src[min(lane + 64u * t, n3 - 1u)];
+        for (int t = 0; t < NL; ++t)  // clamped index: every load in bounds, none predicated
+            v[t] = src[min(lane + 64u * t, nf4 - 1u)];
 #pragma unroll
-        for (int t = 0; t < NF4 / 64; ++t)  // unpredicated (slots past n3 get a copy, never read):
-            stage[lane + 64 * t] = v[t];     // a predicated store would sink its load into the branch
+        for (int t = 0; t < NL; ++t)  // unpredicated (slots past nf4 get a copy, never read):
+            stage[lane + 64 * t] = v[t];  // a predicated store would sink its load into the branch
         wave_lds_sync();
+        const float *sf = reinterpret_cast<const float *>(stage) + lead;
         const uint32_t a = max(e0, cb), b = min(e1, cb + C);
         for (uint32_t e = a; e < b; ++e) {
-            const float4 pa = stage[3 * (e - cb)], pb = stage[3 * (e - cb) + 1];
-            const float pc = reinterpret_cast<const float *>(stage + 3 * (e - cb) + 2)[0];
-            acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
-            acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc;
+            const float *r = sf + kRecF * (e - cb);
+#pragma unroll
+            for (int k = 0; k < kPartial; ++k) acc[k] += r[k];
         }
         wave_lds_sync();
     }
@@ -830,7 +842,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
 // read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
-constexpr int kMultiChunk = 128;  // records per staged chunk (48 B each, per wave): 6 KB of LDS
+constexpr int kMultiChunk = 128;  // records per staged chunk (36 B each, per wave)
+constexpr int kMultiStageF4 = 5 * 64;  // float4 of a wave's staged chunk (RecChunk): 5 KB of LDS
 #ifndef GSR_MV_WPE
 #define GSR_MV_WPE 0  // waves per SIMD the register budget is held to (0: the compiler's choice)
 #endif
@@ -843,20 +856,23 @@ template <int MC>
 constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_stride(MC) + 3) & ~size_t(3)) : 0; }
 template <int MC>
 constexpr size_t multi_lds_bytes() {
-    return sizeof(float) * multi_sh_floats<MC>() + sizeof(float4) * 3 * kMultiChunk * (kShBlock / 64);
+    return sizeof(float) * multi_sh_floats<MC>() + sizeof(float4) * kMultiStageF4 * (kShBlock / 64);
 }
 
 // The lane's share of one record chunk [cb, min(cb + 128, E1)): six float4 held in named registers
 // (an array live across the view loop's control flow stays in scratch memory).  Clamped index:
 // every load in bounds, none predicated.
-struct RecChunk { float4 b0, b1, b2, b3, b4, b5; };
+struct RecChunk { float4 b0, b1, b2, b3, b4; };
+static_assert(rec_chunk_f4(128) <= 5 * 64, "RecChunk holds a 128-record chunk");
 __device__ inline RecChunk mv_load(const float4 *__restrict__ part, uint32_t cb, uint32_t E1, int lane) {
-    const uint32_t n3 = 3u * min(128u, E1 - cb);
-    const float4 *src = part + 3 * (size_t)cb;
+    const size_t f0 = (size_t)kRecF * cb;
+    const uint32_t lead = (uint32_t)(f0 & 3u);
+    const uint32_t nf4 = (lead + kRecF * min(128u, E1 - cb) + 3u) / 4u;
+    const float4 *src = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(part) + (f0 - lead));
     RecChunk c;
-    c.b0 = src[min(lane + 0u, n3 - 1u)];   c.b1 = src[min(lane + 64u, n3 - 1u)];
-    c.b2 = src[min(lane + 128u, n3 - 1u)]; c.b3 = src[min(lane + 192u, n3 - 1u)];
-    c.b4 = src[min(lane + 256u, n3 - 1u)]; c.b5 = src[min(lane + 320u, n3 - 1u)];
+    c.b0 = src[min(lane + 0u, nf4 - 1u)];   c.b1 = src[min(lane + 64u, nf4 - 1u)];
+    c.b2 = src[min(lane + 128u, nf4 - 1u)]; c.b3 = src[min(lane + 192u, nf4 - 1u)];
+    c.b4 = src[min(lane + 256u, nf4 - 1u)];
     return c;
 }
 
@@ -864,7 +880,7 @@ template <int MC>  // SH coefficient count (1, 4, 9, 16), or 0 without SH (colou
 __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const MultiArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
-    float4 *stage = reinterpret_cast<float4 *>(s_sh + multi_sh_floats<MC>()) + (threadIdx.x >> 6) * (3 * kMultiChunk);
+    float4 *stage = reinterpret_cast<float4 *>(s_sh + multi_sh_floats<MC>()) + (threadIdx.x >> 6) * kMultiStageF4;
     const int P = a.P;
     const int i0 = blockIdx.x * kShBlock;
     const int nrow = min(kShBlock, P - i0);
@@ -927,7 +943,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if (E0 < E1 && !have) buf = mv_load(V.part, E0, E1, lane);
         for (uint32_t cb = E0; cb < E1; cb += kMultiChunk) {  // wave-collective
             stage[lane] = buf.b0; stage[lane + 64] = buf.b1; stage[lane + 128] = buf.b2;
-            stage[lane + 192] = buf.b3; stage[lane + 256] = buf.b4; stage[lane + 320] = buf.b5;
+            stage[lane + 192] = buf.b3; stage[lane + 256] = buf.b4;
             have = false;
             if (cb + kMultiChunk < E1) {
                 buf = mv_load(V.part, cb + kMultiChunk, E1, lane);
@@ -941,11 +957,11 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             }
             wave_lds_sync();
             const uint32_t lo = max(e0, cb), hi = min(e1, cb + kMultiChunk);
+            const float *sf = reinterpret_cast<const float *>(stage) + ((kRecF * cb) & 3u);
             for (uint32_t e = lo; e < hi; ++e) {
-                const float4 pa = stage[3 * (e - cb)], pb = stage[3 * (e - cb) + 1];
-                const float pc = reinterpret_cast<const float *>(stage + 3 * (e - cb) + 2)[0];
-                acc[0] += pa.x; acc[1] += pa.y; acc[2] += pa.z; acc[3] += pa.w;
-                acc[4] += pb.x; acc[5] += pb.y; acc[6] += pb.z; acc[7] += pb.w; acc[8] += pc;
+                const float *r = sf + kRecF * (e - cb);
+#pragma unroll
+                for (int k = 0; k < kPartial; ++k) acc[k] += r[k];
             }
             wave_lds_sync();
         }

@@ -17,6 +17,7 @@ constexpr int kTileW = 16;  // 16x16 pixel tiles (upstream BLOCK_X/BLOCK_Y)
 constexpr int kTileH = 16;
 constexpr int kTilePix = kTileW * kTileH;  // 256 = 4 wave64 per tile block
 constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D xy, dconic abc, dopacity, dcolour rgb
+constexpr int kRecF = kPartial;  // floats per stored partial-gradient record (36 bytes, packed)
 constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
 __host__ __device__ inline uint64_t pair_key(uint4 r) { return ((uint64_t)r.y << 32) | r.x; }
 constexpr int kFwdSortCap = 1024;  // lists up to this length are depth-sorted inside k_render_fwd
@@ -171,17 +172,18 @@ struct BinningLayout {
 // BINNING arrays (at BinningLayout(K).total), built by the forward.
 __host__ __device__ inline size_t bwd_items_bytes(int K, int T) { return align256(sizeof(uint2) * (max_bwd_items(K, T) + 1)); }
 
-// SCRATCH (backward): one 48-byte partial-gradient record per Gaussian-tile pair, stored at the
-// pair's EMISSION index (Gaussian-major), so each Gaussian's records are contiguous for the
-// per-Gaussian reduction: (dmean2D.xy, dconic.a, dconic.b) (dconic.c, dopacity, dcolour.rg)
-// (dcolour.b, -, -, -); then the backward's work items ([0].x = count, then (tile, segment) in
-// dispatch order, built by k_bwd_items).
+// SCRATCH (backward): one packed 36-byte partial-gradient record per Gaussian-tile pair, stored at
+// the pair's EMISSION index (Gaussian-major), so each Gaussian's records are contiguous for the
+// per-Gaussian reduction: dmean2D.xy, dconic.abc, dopacity, dcolour.rgb; then the backward's work
+// items ([0].x = count, then (tile, segment) in dispatch order, built by k_bwd_items).
 struct ScratchLayout {
     size_t part, items, total;
     __host__ __device__ ScratchLayout(int K, int T) {
         const size_t k = size_t(K > 0 ? K : 1);
         size_t o = 0;
-        part = o;  o = align256(o + sizeof(float4) * 3 * k);
+        // kRecF floats per record, packed; + 16 bytes: the readers' aligned float4 loads may run up
+        // to 12 bytes past the last record
+        part = o;  o = align256(o + sizeof(float) * kRecF * k + 16);
         items = o; o += bwd_items_bytes(K, T);
         total = o;
     }
