@@ -277,10 +277,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 
 
 def _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused, accumulate_into,
-                  skip=()):
+                  skip=(), overwrite=()):
     """The 8 gradient outputs of the backward (output order) and the accumulate bits: a given
     ``accumulate_into`` tensor is used in place, every other output is allocated (``skip``: output
-    slots not produced at all, returned as None)."""
+    slots not produced at all, returned as None; ``overwrite``: slots whose given tensor receives the
+    gradient without being read, i.e. no accumulate bit)."""
     e = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731 - every element is written
     has = lambda t: t is not None and t.numel() > 0  # noqa: E731
     keep_col = not skip_unused or has(colors)
@@ -290,7 +291,7 @@ def _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unus
               (P, M, 3), (P, 3) if keep_sr else (0,), (P, 4) if keep_sr else (0,)]
     acc = list(accumulate_into or ()) + [None] * 8
     out = []
-    acc_bits = 0
+    acc_bits = given = 0
     for k, shp in enumerate(shapes):  # outputs that accumulate into a caller tensor are not allocated
         t = acc[k]
         if k in skip:
@@ -302,12 +303,14 @@ def _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unus
         if tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous() or t.device != dev:
             raise RuntimeError(f"accumulate_into[{k}]: expected a contiguous float32 {shp} tensor on {dev}")
         out.append(t)
-        acc_bits |= 1 << k
+        given |= 1 << k
+        if k not in overwrite:
+            acc_bits |= 1 << k
     out = tuple(out)
-    if acc_bits:  # the kernel writes caller tensors on this stream: the allocator must not recycle
+    if given:  # the kernel writes caller tensors on this stream: the allocator must not recycle
         cs = torch.cuda.current_stream(dev)  # them before it is done (views on several streams)
         for k in range(8):
-            if acc_bits >> k & 1:
+            if given >> k & 1:
                 out[k].record_stream(cs)
     return out, acc_bits
 
@@ -374,7 +377,7 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
 
 def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations, scale_modifier,
                                        cov3D_precomp, sh, degree, activations=0, skip_unused=True,
-                                       accumulate_into=None):
+                                       accumulate_into=None, overwrite=()):
     """The per-Gaussian half over several views of the same Gaussians (gsr_backward_gaussians), on the
     current stream: returns the 8 gradients of ``rasterize_gaussians_backward`` summed over the views
     (slot 0, dL/dmeans2D, is None: each view's goes to its own array).  ``views``: dicts with the
@@ -382,14 +385,16 @@ def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations
     ``campos``, ``bg``, its ``radii``, ``geomBuffer``, ``scratch`` (from
     ``rasterize_gaussians_backward_render``) and ``num_rendered``, and optionally ``means2D_grad``, a
     contiguous (P, 3) fp32 tensor receiving its screen-space gradient (added into when
-    ``accumulate_means2D``).  The caller orders the views' render halves before this call."""
+    ``accumulate_means2D``).  ``overwrite``: output slots whose ``accumulate_into`` tensor is written
+    without being read (a fresh, uninitialised gradient).  The caller orders the views' render halves
+    before this call."""
     L = load_library()
     keep = []
     dev = means3D.device
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=dev), scales, rotations,
                          scale_modifier, cov3D_precomp, keep, activations)
     out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
-                                  accumulate_into, skip=(0,))
+                                  accumulate_into, skip=(0,), overwrite=overwrite)
     if P == 0 or not views:
         return out
     cams = []

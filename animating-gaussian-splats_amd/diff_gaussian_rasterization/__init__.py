@@ -79,7 +79,8 @@ def _accumulation_target(t, node=None, create=False):
     the gradient (``create_graph``).  Gives the same value as autograd's AccumulateGrad (one fp32
     add, ``grad += new``) without its separate read-read-write pass; every other case returns the
     gradient to autograd as stock Functions do.  ``create``: a leaf that qualifies but has no
-    ``.grad`` yet gets a zero one (0 + g is what AccumulateGrad would have stored)."""
+    ``.grad`` yet comes back as ``_Fresh(leaf)``: its gradient is allocated (uninitialised) when the
+    deferred pass runs and written there without a read (what AccumulateGrad would have stored)."""
     if t is None or not isinstance(t, torch.Tensor) or t.numel() == 0 or not t.is_leaf or not t.requires_grad:
         return None
     g = t.grad
@@ -92,8 +93,40 @@ def _accumulation_target(t, node=None, create=False):
     if torch.is_grad_enabled() or not _engine_accumulates(t, node):
         return None
     if g is None:
-        t.grad = g = torch.zeros_like(t)
+        if not _defer["fresh"]:  # (A/B switch: zero-filled gradient, read back by the pass)
+            t.grad = g = torch.zeros_like(t)
+            return g
+        return _Fresh(t)
     return g
+
+
+class _Fresh:
+    """A deferred gradient target whose leaf had no ``.grad``: instead of a zero fill that the
+    per-Gaussian pass would read back, the flush allocates it and the first launch writing it
+    overwrites it."""
+    __slots__ = ("leaf",)
+
+    def __init__(self, leaf):
+        self.leaf = leaf
+
+
+def _fresh_target(t, created, post):
+    """Resolve a deferred target at the flush -> (tensor, overwrite).  ``created``: ids of leaves
+    whose .grad this flush allocated and no launch has written yet; ``post``: (leaf, tensor) pairs
+    to add into a .grad that appeared meanwhile in an unusable form."""
+    if not isinstance(t, _Fresh):
+        return t, False
+    leaf = t.leaf
+    g = leaf.grad
+    if g is None:  # still absent: allocate, the first writer overwrites
+        leaf.grad = g = torch.empty_like(leaf, memory_format=torch.contiguous_format)
+        created.add(id(leaf))
+    elif id(leaf) not in created and (g.dtype != torch.float32 or not g.is_contiguous() or
+                                      g.shape != leaf.shape or g.requires_grad):
+        tmp = torch.zeros_like(leaf, memory_format=torch.contiguous_format)  # set by autograd meanwhile
+        post.append((leaf, tmp))
+        return tmp, False
+    return g, id(leaf) in created
 
 
 # ---- deferred multi-view per-Gaussian backward ------------------------------------------------
@@ -109,7 +142,8 @@ def _accumulation_target(t, node=None, create=False):
 # are keyed by the engine's graph-task id; a pass that raises never runs its callback, and the next
 # flush drops its views -- so backward passes through this path must not run concurrently from
 # several threads (set_deferred_backward(False) for that).
-_defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0"}
+_defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0",
+          "fresh": os.environ.get("GSR_FRESH_GRADS", "1") != "0"}
 _pending_lock = threading.Lock()
 _pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
 _queued = set()  # graph tasks whose flush callback is queued
@@ -131,6 +165,7 @@ def _flush_pending():
         for k in [k for k in _pending if k[0] <= task]:
             del _pending[k]
         _queued.discard(task)
+    created, post = set(), []
     for grp in groups:
         dev = grp["device"]
         with torch.cuda.device(dev):
@@ -139,9 +174,24 @@ def _flush_pending():
                 if s != cur:
                     cur.wait_stream(s)
             (means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act) = grp["gauss"]
-            _C.rasterize_gaussians_backward_views(grp["views"], means3D, colors, scales, rotations,
+            targets, over = [None] * 8, []
+            for k in range(1, 8):
+                targets[k], ow = _fresh_target(grp["targets"][k], created, post)
+                if ow:
+                    over.append(k)
+            views = []
+            for v in grp["views"]:  # each view's screen-space gradient: overwrite a fresh one first
+                m2, ow = _fresh_target(v["means2D_grad"], created, post)
+                views.append(dict(v, means2D_grad=m2, accumulate_means2D=not ow))
+                if ow:
+                    created.discard(id(v["means2D_grad"].leaf))
+            _C.rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations,
                                                   scale_modifier, cov3D, sh, degree, activations=act,
-                                                  skip_unused=True, accumulate_into=grp["targets"])
+                                                  skip_unused=True, accumulate_into=targets, overwrite=over)
+            for k in over:  # written: later launches add into it
+                created.discard(id(grp["targets"][k].leaf))
+    for leaf, tmp in post:
+        leaf.grad = leaf.grad + tmp
 
 
 def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn):
@@ -171,8 +221,9 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
     rs = ctx.raster_settings
     scratch = render_fn()
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else 0  # noqa: E731
+    tkey = lambda t: ("fresh", id(t.leaf)) if isinstance(t, _Fresh) else ptr(t)  # noqa: E731
     key = (means3D.device, P, ptr(means3D), ptr(scales), ptr(rotations), ptr(cov3D), ptr(sh), ptr(colors),
-           int(degree), float(scale_modifier), int(act)) + tuple(ptr(t) for t in targets[1:])
+           int(degree), float(scale_modifier), int(act)) + tuple(tkey(t) for t in targets[1:])
     view = {"viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix, "tanfovx": rs.tanfovx,
             "tanfovy": rs.tanfovy, "image_height": rs.image_height, "image_width": rs.image_width,
             "campos": rs.campos, "bg": rs.bg, "radii": radii, "geomBuffer": geomBuffer, "scratch": scratch,

@@ -237,3 +237,30 @@ def test_workspaces_freed_without_the_cyclic_collector(cuda):
                 set_deferred_backward(prev)
     finally:
         gc.enable()
+
+
+def test_deferred_fresh_grad_with_a_second_path(cuda):
+    """Leaves without a .grad get theirs allocated at the end of the pass and overwritten by the first
+    launch (no zero fill): also when another term of the loss reaches the same leaves during the pass
+    (autograd's AccumulateGrad sets .grad first, the deferred pass then adds into it) and over two
+    launch groups (10 views)."""
+    a, deg = _inputs(cuda, "sh3")
+    cams = _cams(cuda, 10, deg)
+    dls = [S.upstream_grad(H, W, seed=140 + k, device=cuda) for k in range(len(cams))]
+
+    def run(deferred):
+        leaves = _leaves(a)
+        prev = set_deferred_backward(deferred)
+        try:
+            loss = _views_loss(leaves, cams, dls) + 0.5 * (leaves["means3D"] ** 2).sum() + leaves["opacities"].sum()
+            loss.backward()
+        finally:
+            set_deferred_backward(prev)
+        torch.cuda.synchronize()
+        return {k: v.grad.clone() for k, v in leaves.items() if v.grad is not None}
+
+    ref, got = run(False), run(True)
+    assert set(ref) == set(got)
+    for k in ref:
+        assert torch.isfinite(got[k]).all(), k
+        _close(k, got[k], ref[k])
