@@ -715,10 +715,15 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     constexpr int kQW = kTileW, kQH = 4;
 #endif
     const bool inside = px < W && py < H;
-    bool done = !inside;
+    // The pixel's alpha threshold: 1/255 while it blends, 2 (above any alpha <= 0.99) once it is done
+    // (outside the image, or saturated): a finished pixel fails the same compare instead of carrying
+    // a done flag through the loop as a lane mask (its mask logic cost ~7 scalar instructions per
+    // blended entry).  The decisions are those of !done && blend_ok(e).
+    constexpr float kThrDone = 2.0f;
+    float thr = inside ? 1.0f / 255.0f : kThrDone;
     if (threadIdx.x == 0) s_live = 0;
     __syncthreads();  // sort outputs consumed / s_live cleared
-    if (__ballot(!done) && lane == 0) atomicOr(&s_live, 1u << wv);
+    if (__ballot(thr < kThrDone) && lane == 0) atomicOr(&s_live, 1u << wv);
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
     uint32_t last = 0;
 #if GSR_FWD_PREFETCH
@@ -785,14 +790,13 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         uint64_t m = __ballot((s_u.st.q[lane] >> wv) & 1u);
         if (!((live >> wv) & 1u)) m = 0;
         // one entry's blend into this pixel's state (front to back)
-        auto take = [&](const Blend &e, float4 b, float4 c, int j, bool valid) {
-            const bool ok = valid && !done && blend_ok(e);
+        auto take = [&](const Blend &e, float4 b, float4 c, int j) {
+            const bool ok = e.p2 <= 0.0f && e.alpha >= thr;  // blend_ok(e) for a live pixel
             const float test_T = fmaf(-e.alpha, Tt, Tt);  // T (1 - alpha), one rounding
             // keep == !(test_T < 1e-4) (test_T is never NaN: T in (0, 1], alpha in [0, 0.99]); the
-            // pixel finishes when it takes the entry but may not keep it: (done | ok) & ~use, one
-            // compare and mask logic instead of a second compare
+            // pixel finishes when it takes the entry but may not keep it
             const bool use = ok && test_T >= 0.0001f;
-            done = (done || ok) && !use;
+            thr = (ok && !use) ? kThrDone : thr;
             const float w = use ? e.alpha * Tt : 0.f;
             C0 = fmaf(c.x, w, C0);
             C1 = fmaf(c.y, w, C1);
@@ -805,9 +809,9 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const int j = __builtin_ctzll(m);
             m &= m - 1;
             const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
-            take(blend_eval(a, b, pfx, pfy), b, c, j, true);
+            take(blend_eval(a, b, pfx, pfy), b, c, j);
         }
-        if (((live >> wv) & 1u) && !__ballot(!done) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
+        if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
     if (inside) {
         const int pid = py * W + px;
