@@ -54,3 +54,28 @@ def test_inputs_subset_is_respected():
 
     F.apply(a, c).backward(inputs=[c])  # only c's AccumulateGrad runs
     assert seen["will"] == [False, True]
+
+
+def test_fresh_targets_resolve_at_the_flush():
+    """Deferred targets of leaves without .grad (D._Fresh): the flush allocates the gradient and the
+    first launch overwrites it; a later launch of the same flush adds into it; a .grad that autograd
+    set meanwhile is added into in place, or -- in a form the kernel cannot write -- through a
+    temporary added afterwards (CPU test of the bookkeeping)."""
+    created, post = set(), []
+    a = torch.zeros(4, 3, requires_grad=True)
+    g, ow = D._fresh_target(D._Fresh(a), created, post)
+    assert ow and g is a.grad and g.shape == a.shape and g.is_contiguous()
+    created.discard(id(a))  # the first launch wrote it
+    g2, ow2 = D._fresh_target(D._Fresh(a), created, post)
+    assert g2 is g and not ow2 and not post
+    b = torch.zeros(4, 3, requires_grad=True)
+    b.grad = torch.ones(4, 3)  # set by AccumulateGrad during the pass
+    gb, owb = D._fresh_target(D._Fresh(b), created, post)
+    assert gb is b.grad and not owb and not post
+    c = torch.zeros(4, 3, requires_grad=True)
+    c.grad = torch.ones(3, 4).t()  # non-contiguous: a temporary, added after the launch
+    gc, owc = D._fresh_target(D._Fresh(c), created, post)
+    assert gc is not c.grad and not owc and post == [(c, gc)] and not gc.any()
+    t = torch.ones(4, 3)
+    assert D._fresh_target(t, created, post) == (t, False)  # an existing target passes through
+    assert D._fresh_target(None, created, post) == (None, False)
