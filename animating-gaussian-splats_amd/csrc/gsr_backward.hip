@@ -914,6 +914,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     for (int k = 0; k < (RL > 0 ? RL : 1); ++k) gsh[k] = 0.f;
     bool vis = false;
     float o_act = 0.f;  // the activated opacity, from the record of a view that sees the Gaussian
+    float m2[3] = {0.f, 0.f, 0.f};  // the screen-space gradient carried across views of one array
     const int active = (a.D + 1) * (a.D + 1);
     // each view's emission span and radius are loaded one view ahead (their latency then hides
     // behind the previous view's records and chains instead of opening every view)
@@ -968,11 +969,19 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if (!live) continue;
         const bool r = rv > 0;
         if (V.dL_dmeans2D) {
-            float o2[3];
-            old_load(V.dL_dmeans2D, 3 * (size_t)i, V.acc2, o2);
-            gput_old(V.dL_dmeans2D, 3 * i, r ? acc[0] : 0.f, V.acc2, o2[0]);
-            gput_old(V.dL_dmeans2D, 3 * i + 1, r ? acc[1] : 0.f, V.acc2, o2[1]);
-            gput_old(V.dL_dmeans2D, 3 * i + 2, 0.f, V.acc2, o2[2]);
+            // consecutive views writing the same array (one means2D leaf rendered from several
+            // cameras) carry its value in registers: loaded at the run's first view, stored after its
+            // last -- the same additions, in view order, as a read-modify-write per view
+            const bool cont = v > 0 && a.v[v - 1].dL_dmeans2D == V.dL_dmeans2D;
+            const bool last = !(v + 1 < a.nv && a.v[v + 1].dL_dmeans2D == V.dL_dmeans2D);
+            const float gx = r ? acc[0] : 0.f, gy = r ? acc[1] : 0.f;
+            if (!cont) old_load(V.dL_dmeans2D, 3 * (size_t)i, V.acc2, m2);
+            m2[0] = V.acc2 ? m2[0] + gx : gx;
+            m2[1] = V.acc2 ? m2[1] + gy : gy;
+            m2[2] = V.acc2 ? m2[2] + 0.f : 0.f;
+            if (last) {
+                V.dL_dmeans2D[3 * i] = m2[0]; V.dL_dmeans2D[3 * i + 1] = m2[1]; V.dL_dmeans2D[3 * i + 2] = m2[2];
+            }
         }
         if (!r) continue;
         // the activated opacity (sigmoid chain only): written by every view that sees the Gaussian
