@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import threading
+import weakref
 from typing import NamedTuple
 
 import torch
@@ -23,7 +24,7 @@ from torch.autograd.graph import get_gradient_edge
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_parameters", "set_deferred_backward"]
+           "rasterize_parameters", "set_deferred_backward", "pending_views", "clear_pending"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -139,9 +140,13 @@ def _fresh_target(t, created, post):
 # Gaussians (gsr_backward_gaussians), reading the parameters and read-modify-writing every gradient
 # array once instead of once per view.  .grad holds the summed result when backward() returns, as
 # with stock autograd; the fp32 additions are grouped differently (views summed first).  Queued views
-# are keyed by the engine's graph-task id; a pass that raises never runs its callback, and the next
-# flush drops its views -- so backward passes through this path must not run concurrently from
-# several threads (set_deferred_backward(False) for that).
+# are keyed by the engine's graph-task id and each pass flushes only its own: a reentrant backward
+# inside the pass (torch.utils.checkpoint(use_reentrant=True)) or a pass run concurrently from another
+# thread is a different graph task with its own views and callback.  A pass that raises never runs
+# its callback; the engine then destroys the callback object, whose finalizer drops that pass's
+# queued views (and the SCRATCH buffers they hold) at once.  AccumulateGrad *node* hooks
+# (node.register_hook / register_prehook, e.g. DDP's reducer) cannot be seen from Python: such
+# callers read .grad during the pass and must run with set_deferred_backward(False).
 _defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0",
           "fresh": os.environ.get("GSR_FRESH_GRADS", "1") != "0"}
 _pending_lock = threading.Lock()
@@ -156,42 +161,85 @@ def set_deferred_backward(on: bool) -> bool:
     return prev
 
 
-def _flush_pending():
-    """Final callback of a backward pass: one per-Gaussian pass per group of queued views.  Groups
-    of older passes that never flushed (a pass that raised) are dropped."""
-    task = torch._C._current_graph_task_id()
+def pending_views() -> int:
+    """Views queued for a deferred per-Gaussian pass that has not run yet (0 between backward passes)."""
+    with _pending_lock:
+        return sum(len(g["views"]) for g in _pending.values())
+
+
+def clear_pending() -> None:
+    """Drop every queued view (their SCRATCH buffers are freed); a pass still running loses them."""
+    with _pending_lock:
+        _pending.clear()
+        _queued.clear()
+
+
+def _drop_task(task):
+    with _pending_lock:
+        for k in [k for k in _pending if k[0] == task]:
+            del _pending[k]
+        _queued.discard(task)
+
+
+class _TaskFlush:
+    """The end-of-pass callback of one graph task.  The engine holds the only reference: after a
+    successful pass it has run (and flushed the task's views); after a pass that raised it is
+    released without running, and the finalizer registered beside it drops the task's views."""
+    __slots__ = ("task", "__weakref__")
+
+    def __init__(self, task):
+        self.task = task
+
+    def __call__(self):
+        _flush_pending(self.task)
+
+
+def _queue_flush(task):
+    """Queue ``task``'s end-of-pass flush on the running backward pass (once per pass)."""
+    cb = _TaskFlush(task)
+    weakref.finalize(cb, _drop_task, task)
+    torch.autograd.Variable._execution_engine.queue_callback(cb)
+
+
+def _flush_pending(task):
+    """Final callback of a backward pass: one per-Gaussian pass per group of this pass's views."""
     with _pending_lock:
         groups = [g for (t, _), g in _pending.items() if t == task]
-        for k in [k for k in _pending if k[0] <= task]:
+        for k in [k for k in _pending if k[0] == task]:
             del _pending[k]
         _queued.discard(task)
     created, post = set(), []
     for grp in groups:
-        dev = grp["device"]
-        with torch.cuda.device(dev):
-            cur = torch.cuda.current_stream(dev)
-            for s in grp["streams"]:  # every view's render half precedes the per-Gaussian pass
-                if s != cur:
-                    cur.wait_stream(s)
-            (means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act) = grp["gauss"]
-            targets, over = [None] * 8, []
-            for k in range(1, 8):
-                targets[k], ow = _fresh_target(grp["targets"][k], created, post)
-                if ow:
-                    over.append(k)
-            views = []
-            for v in grp["views"]:  # each view's screen-space gradient: overwrite a fresh one first
-                m2, ow = _fresh_target(v["means2D_grad"], created, post)
-                views.append(dict(v, means2D_grad=m2, accumulate_means2D=not ow))
-                if ow:
-                    created.discard(id(v["means2D_grad"].leaf))
-            _C.rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations,
-                                                  scale_modifier, cov3D, sh, degree, activations=act,
-                                                  skip_unused=True, accumulate_into=targets, overwrite=over)
-            for k in over:  # written: later launches add into it
-                created.discard(id(grp["targets"][k].leaf))
+        _run_group(grp, created, post)
     for leaf, tmp in post:
         leaf.grad = leaf.grad + tmp
+
+
+def _run_group(grp, created, post):
+    """One multi-view per-Gaussian pass over a group of queued views of the same Gaussians."""
+    dev = grp["device"]
+    with torch.cuda.device(dev):
+        cur = torch.cuda.current_stream(dev)
+        for s in grp["streams"]:  # every view's render half precedes the per-Gaussian pass
+            if s != cur:
+                cur.wait_stream(s)
+        (means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act) = grp["gauss"]
+        targets, over = [None] * 8, []
+        for k in range(1, 8):
+            targets[k], ow = _fresh_target(grp["targets"][k], created, post)
+            if ow:
+                over.append(k)
+        views = []
+        for v in grp["views"]:  # each view's screen-space gradient: overwrite a fresh one first
+            m2, ow = _fresh_target(v["means2D_grad"], created, post)
+            views.append(dict(v, means2D_grad=m2, accumulate_means2D=not ow))
+            if ow:
+                created.discard(id(v["means2D_grad"].leaf))
+        _C.rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations,
+                                              scale_modifier, cov3D, sh, degree, activations=act,
+                                              skip_unused=True, accumulate_into=targets, overwrite=over)
+        for k in over:  # written: later launches add into it
+            created.discard(id(grp["targets"][k].leaf))
 
 
 def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn):
@@ -240,7 +288,7 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
         queue = task not in _queued
         _queued.add(task)
     if queue:
-        torch.autograd.Variable._execution_engine.queue_callback(_flush_pending)
+        _queue_flush(task)
     return True
 
 

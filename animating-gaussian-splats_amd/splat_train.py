@@ -10,9 +10,9 @@ create_render_arguments + Renderer (image)  :110-126    rasterize_parameters (ac
 0.8 l1 + 0.2 (1 - calc_ssim)                :127-129    splat_loss.image_loss (fused L1 + SSIM)
 segmentation render + loss                  :132-151    rasterize_parameters(colors = masks) + loss
 update_max_2d_radii_and_visibility_mask     :154-162    splat_densify (statistics kernel)
-total_loss.backward()                       :247        same (native backward kernels)
-densify_gaussians                           :249-255    splat_densify.densify_gaussians
-optimizer.step(); zero_grad(set_to_none)    :256-257    splat_adam.FusedAdam (one launch)
+total_loss.backward()                       :237        same (native backward kernels)
+densify_gaussians                           :239-245    splat_densify.densify_gaussians
+optimizer.step(); zero_grad(set_to_none)    :246-247    splat_adam.FusedAdam (one launch)
 =====================================================  ============================================
 
 ``View`` restates shared.py:13-18.  The image-render ``means2D`` is a leaf that receives the same

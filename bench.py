@@ -89,12 +89,14 @@ def pipeline_bytes(P, K, N, T, F, sh):
     return P * (220 + 3 * F + 12 * sh) + 120 * K + 44 * N + 16 * T
 
 
-def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu):
-    """The C oracle (OpenMP over tiles / Gaussians, OMP_NUM_THREADS threads), forward + backward of ONE
-    view of the same workload on this host's cores."""
+def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu, threads=0):
+    """The C oracle (OpenMP over tiles / Gaussians), forward + backward of ONE view of the same
+    workload on this host's cores: ``threads`` OpenMP threads, 0 = every CPU this process may run on
+    (os.sched_getaffinity, what `nproc` reports)."""
     from oracle import oracle as O
     import splat_scenes as S
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = O.set_threads(threads if threads > 0 else avail)
     a = {k: (v.detach().numpy() if isinstance(v, torch.Tensor) else v)
          for k, v in S.activated_inputs(params_cpu, cfg.sh_degree).items()}
     t0 = time.perf_counter()
@@ -105,11 +107,11 @@ def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu):
     O.backward(st, dl_cpu.numpy())
     dt = time.perf_counter() - t0
     return {"value": round(cfg.P / dt / 1e6, 6), "unit": "Msplats/s", "cores": threads, "kind": "port",
-            "host_nproc": os.cpu_count(),
+            "host_nproc": os.cpu_count(), "available_cpus": avail,
             "sample": f"1 view of the same workload ({cfg.P} Gaussians, {cam_cpu.image_width}x"
                       f"{cam_cpu.image_height}, SH{cfg.sh_degree}) fwd+bwd by the C oracle "
-                      f"(oracle/gsr_oracle.c, OpenMP, {threads} threads of {os.cpu_count()} host CPUs), "
-                      f"{dt:.2f} s"}
+                      f"(oracle/gsr_oracle.c, OpenMP, {threads} threads; {avail} CPUs available to the "
+                      f"process, {os.cpu_count()} on the host), {dt:.2f} s"}
 
 
 def _torch_calc_ssim(img1, img2):
@@ -452,22 +454,98 @@ def _dry_run(args, rank, world):
         dist.destroy_process_group()
 
 
+def train_call_site(steps, cfg, cams, views, dl, dev, streams, sh):
+    """train.py's render call site driven exactly as an unchanged train.py drives it (outside
+    ``value``): the Gaussian parameters are frozen (train.py:155-163 loads them with requires_grad =
+    False); the means and rotations of the step are ``p.detach()`` copies plus 0.01 x a deformation
+    output (train.py:297-308; here a (P, 7) leaf stands in for the network, which is out of scope);
+    every view builds its arguments with create_render_arguments (shared.py:29-42: normalize / sigmoid
+    / exp and a fresh ``zeros_like(requires_grad=True) + 0`` means2D); the view losses are summed and
+    backpropagated once (train.py:402-418, 767).  The rasterizer's inputs are therefore NOT leaves and
+    every view takes the immediate per-view backward (no deferred multi-view pass).  Same streams and
+    per-stream submitting threads as the headline.  ``sh``: False = the reference's colors_precomp (RGB,
+    what train.py renders), True = SH3 coefficients passed as ``shs`` (the headline's features)."""
+    import splat_scenes as S
+    import splat_step
+    from diff_gaussian_rasterization import _C
+    P = cfg.P
+    base = S.synthetic_cloud(P, cfg.s0, sh_degree=3 if sh else -1, seed=0, device=dev)  # requires_grad False
+    delta = torch.zeros(P, 7, device=dev, requires_grad=True)
+    cur = {}
+    main = torch.cuda.current_stream(dev)
+
+    def args_of(_ci):  # shared.py:29-42 on the step's updated parameters, per view
+        a = S.render_arguments(cur["p"])
+        if sh:
+            a.pop("colors_precomp")
+            a["shs"] = cur["p"]["shs"]
+        return a
+
+    rstep = splat_step.RenderStep(dev, cams, args_of, dl, streams, threads=True)
+
+    def one(it):
+        p = dict(base)  # update_gaussian_cloud_parameters (train.py:297-308)
+        p["means"] = base["means"].clone()
+        p["means"] += delta[:, :3] * 0.01
+        p["rotation_quaternions"] = base["rotation_quaternions"].clone()
+        p["rotation_quaternions"] += delta[:, 3:] * 0.01
+        cur["p"] = p
+        for s in streams:
+            s.wait_stream(main)  # the step's updated parameters
+        rstep(views(it))
+        for s in streams:
+            main.wait_stream(s)
+        delta.grad = None  # optimizer.zero_grad()
+
+    for it in range(3):
+        one(it)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for it in range(steps):
+        one(3 + it)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / steps * 1e3
+    # per-kernel device times of the same path (one stream, events on every phase; untimed)
+    _C.profile_reset()
+    _C.profile_select(None)
+    _C.profile_enable(True)
+    for it in range(2):
+        p = dict(base)
+        p["means"] = base["means"] + delta[:, :3] * 0.01
+        p["rotation_quaternions"] = base["rotation_quaternions"] + delta[:, 3:] * 0.01
+        cur["p"] = p
+        rstep(views(it), solo=True)
+        delta.grad = None
+    torch.cuda.synchronize()
+    _C.profile_enable(False)
+    phases = {ph: _C.profile_read(ph) for ph in PHASES}
+    rstep.close()
+    nv = len(views(0))
+    return {"features": "SH3 (shs)" if sh else "RGB (colors_precomp, as train.py renders)",
+            "ms_per_step": round(ms, 4), "views_per_step": nv, "Msplats_per_s": round(nv * P / ms / 1e3, 2),
+            "inputs": "non-leaf (frozen Gaussians, means/rotations = detach + 0.01 delta, per-view activations)",
+            "backward": "immediate per-view (rasterizer inputs are not leaves)",
+            "solo_phase_ms_per_launch": {ph: round(v[0] / max(v[1], 1), 5) for ph, v in phases.items() if v[1]},
+            "steps": steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="C3", choices=["C3", "C3M", "C4", "C5"],
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 100; C5: 5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warm-up steps (default 10; C5: 1)")
+    ap.add_argument("--config", default="C3", choices=["C2", "C3", "C3M", "C4", "C5"],
                     help="C3 (default): 1M Gaussians SH3 at 1080p, --views-per-rank rig views per GPU per "
+                         "step (weak scaling); C2: 100k Gaussians, RGB, the 4 cameras of 800x800 per GPU per "
                          "step (weak scaling); C4: 1M Gaussians, the 27-camera rig sharded round-robin over "
                          "the ranks per step + one RCCL SUM all-reduce (strong scaling); C5: 2M Gaussians x "
-                         "150-frame sequence, frames sharded in blocks, one per-frame optimisation iteration "
-                         "(5 views, fused L1+SSIM, fused Adam) per GPU per step, no collective (weak scaling); "
-                         "C3M: C3 with half of the means in 16 tight clusters (a densified scene: tiles of "
-                         "tens of thousands of pairs)")
-    ap.add_argument("--views-per-rank", type=int, default=5,
-                    help="C3 / C5: views rendered per GPU per step (train.py:753 optimises on the summed "
-                         "losses of 5 views per step)")
+                         "150-frame sequence, independent per-frame fits sharded in frame blocks, one "
+                         "optimisation iteration (5 views, fused L1+SSIM, fused Adam) of every frame per step, "
+                         "no collective (strong scaling); C3M: C3 with half of the means in 16 tight clusters "
+                         "(a densified scene: tiles of tens of thousands of pairs)")
+    ap.add_argument("--views-per-rank", type=int, default=None,
+                    help="C3 / C5: views rendered per GPU per step / per frame (default 5: train.py:753 "
+                         "optimises on the summed losses of 5 views per step); C2: default 4")
     ap.add_argument("--stream-priority", type=int, default=0,
                     help="HIP priority of the view streams (negative = higher than the main stream, "
                          "which runs the multi-view per-Gaussian pass and the collectives)")
@@ -491,8 +569,13 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / sharding / collective (gloo, no GPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="OpenMP threads of the CPU baseline (0 = every CPU this process may run on, "
+                         "os.sched_getaffinity)")
     ap.add_argument("--call-site-steps", type=int, default=10,
-                    help="steps timed for each train.py call-site variant (0 = skip; N = 1, C3 only)")
+                    help="steps timed for each call-site variant (0 = skip; N = 1, C3 only)")
+    ap.add_argument("--train-steps", type=int, default=10,
+                    help="steps timed for the train.py call-site legs (0 = skip; N = 1, C3 only)")
     ap.add_argument("--loss-steps", type=int, default=10,
                     help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip; N = 1, C3)")
     ap.add_argument("--densify-steps", type=int, default=5,
@@ -502,7 +585,18 @@ def main():
                          "leg (0 = skip; N = 1, C3)")
     ap.add_argument("--probe-steps", type=int, default=3,
                     help="untimed steps with events on every phase (per-kernel breakdown)")
+    ap.add_argument("--grad-checksum", default=None,
+                    help="C2 / C3 / C4: after the timed steps, one more step whose (all-reduced) gradient "
+                         "bucket is saved to PATH.rank<r>.pt with the step's camera indices (a parity hook "
+                         "for the multi-rank path: tests/test_dp_gpu.py)")
     args = ap.parse_args()
+    c5_cfg = args.config == "C5"
+    if args.steps is None:
+        args.steps = 5 if c5_cfg else 100
+    if args.warmup is None:
+        args.warmup = 1 if c5_cfg else 10
+    if args.views_per_rank is None:
+        args.views_per_rank = 4 if args.config == "C2" else 5
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_self_launch(args.gpus))
@@ -519,6 +613,7 @@ def main():
 
     import splat_dp
     import splat_scenes as S
+    import splat_step
     from diff_gaussian_rasterization import GaussianRasterizer, _C, rasterize_parameters
 
     dist = None
@@ -536,8 +631,10 @@ def main():
     torch.cuda.set_device(dev)
     _C.load_library()
 
-    if args.config == "C5":
+    if c5_cfg:
         cfg = S.SceneConfig("C5", 2_000_000, 1920, 1080, 1600.0, 0.005, views=S.RIG27)
+    elif args.config == "C2":
+        cfg = S.CONFIGS["C2"]
     else:
         base = S.CONFIGS["C3" if args.config == "C3M" else args.config]
         cfg = S.SceneConfig(args.config, base.P, base.width, base.height, base.focal, base.s0,
@@ -557,11 +654,11 @@ def main():
     if cfg.sh_degree >= 0:
         act.pop("colors_precomp")
     leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
-    grads_of = lambda: [v.grad for k, v in leaves.items() if k != "means2D"]  # noqa: E731
-    # N > 1 (C3 / C4): the gradients live in one flat bucket that backward accumulates into and RCCL
-    # reduces in place (no pack / unpack copies)
-    reducer = splat_dp.GradAllReduce([v for k, v in leaves.items() if k != "means2D"]).attach() \
-        if dist is not None and args.config != "C5" else None
+    grad_leaves = [v for k, v in leaves.items() if k != "means2D"]
+    grads_of = lambda: [v.grad for v in grad_leaves]  # noqa: E731
+    # N > 1 (C2 / C3 / C4): the gradients live in one flat bucket that backward accumulates into and
+    # RCCL reduces in place (no pack / unpack copies)
+    reducer = splat_dp.GradAllReduce(grad_leaves).attach() if dist is not None and not c5_cfg else None
 
     if args.config == "C4":  # the whole rig every step, sharded round-robin (4,4,4,3,3,3,3,3 at 8)
         views_per_step = len(cams)
@@ -572,7 +669,7 @@ def main():
     else:
         views_per_step = world * V
 
-        def views_of(it):  # rank r renders its round-robin share of this step's world * V rig cameras
+        def views_of(it):  # rank r renders its round-robin share of this step's world * V cameras
             return splat_dp.shard_views([(it * world * V + k) % len(cams) for k in range(world * V)], rank, world)
 
     main_stream = torch.cuda.current_stream(dev)
@@ -584,66 +681,50 @@ def main():
     if reducer is not None:  # the bucket's zeroing (main stream) precedes the first backward
         _C.grad_fence(*grads_of())
 
-    pool = None
     if args.submit == "auto":
         args.submit = "threads" if args.step_shape == "summed" else "serial"
-    if args.submit == "threads" and len(streams) > 1:
-        from concurrent.futures import ThreadPoolExecutor
-        pool = ThreadPoolExecutor(max_workers=len(streams))
+    rstep = splat_step.RenderStep(dev, cams, lambda ci: leaves, dl, streams, threads=args.submit == "threads",
+                                  shape="summed" if args.step_shape == "summed" else "per_view")
 
-    def forward_views(vs, s):  # one stream's share of a summed step's forwards
-        torch.cuda.set_device(dev)
-        with torch.cuda.stream(s):
-            return [GaussianRasterizer(raster_settings=cams[ci])(**leaves)[0] for ci in vs]
-
-    def run_views(vs, s):  # one stream's share of a step, fwd + bwd per view
-        torch.cuda.set_device(dev)
-        with torch.cuda.stream(s):
-            for ci in vs:
-                img, _radii, _depth = GaussianRasterizer(raster_settings=cams[ci])(**leaves)
-                img.backward(dl)
-
-    def step(it, solo=False):
+    def step(it, solo=False, keep=False):
         # No stream waits for another at the step start: libgsr orders the gradient writes across
         # streams, record_stream keeps freed gradients from early reuse, and for N > 1 the bucket's
         # all-reduce + reset on the main stream is declared with grad_fence, so the next step's
         # forwards run during the all-reduce and only its first gradient write waits for it.
-        # solo: one stream, one submitting thread (per-kernel times without concurrency)
-        vs = views_of(it)
-        ns = 1 if solo else len(streams)
-        if args.step_shape == "summed":  # forwards on the streams, then one backward of the summed loss
-            if pool is not None and not solo:  # stream k's views submitted by its own host thread
-                futs = [pool.submit(forward_views, vs[k::ns], streams[k]) for k in range(min(ns, len(vs)))]
-                imgs = [img for f in futs for img in f.result()]
-            else:
-                imgs = []
-                for k, ci in enumerate(vs):
-                    imgs += forward_views([ci], streams[k % ns])
-            torch.autograd.backward(imgs, [dl] * len(imgs))
-            del imgs
-        elif pool is not None:  # view k on stream k % ns, submitted by that stream's thread
-            futs = [pool.submit(run_views, vs[k::ns], streams[k]) for k in range(min(ns, len(vs)))]
-            for f in futs:
-                f.result()
-        else:
-            for k, ci in enumerate(vs):
-                run_views([ci], streams[k % ns])
+        # solo: one stream, one submitting thread (per-kernel times without concurrency); keep: leave
+        # the step's (reduced) gradients in place
+        rstep(views_of(it), solo=solo)
+        for s in streams:
+            main_stream.wait_stream(s)  # the step ends on the main stream (its end event, the reduce)
         if reducer is not None:
-            for s in streams:
-                main_stream.wait_stream(s)
             reducer.reduce()  # one flat-bucket all-reduce (SUM) of every gradient over RCCL
+            if keep:
+                return
             reducer.zero_()
             _C.grad_fence(*grads_of())
             leaves["means2D"].grad = None
-        else:
+        elif not keep:
             for p in leaves.values():
                 p.grad = None
 
-    c5 = None
-    if args.config == "C5":
-        c5 = _C5Fit(cfg, params_cpu, cams, rank, world, V, dev, streams, main_stream,
-                    args.warmup + args.probe_steps + args.steps)
-        step = c5.step  # noqa: F811
+    fits = None
+    if c5_cfg:
+        import splat_adam
+        import splat_frames
+        import splat_loss
+
+        def render(p, cam):
+            return rasterize_parameters(p, cam)[0]
+        fits = splat_frames.FrameFits(
+            {k: v.to(dev) for k, v in params_cpu.items()}, cams, rank, world, V, render, splat_loss.image_loss,
+            lambda p: splat_adam.FusedAdam([{"params": [v], "name": k, "lr": splat_frames.FRAME_LRS.get(k, 1e-3)}
+                                            for k, v in p.items()], lr=0.0, eps=1e-15),
+            streams=streams, main_stream=main_stream)
+        torch.cuda.synchronize()
+        views_per_step = sum(len(splat_dp.shard_frames(150, r, world)) for r in range(world)) * V
+
+        def step(it, solo=False, keep=False):  # noqa: F811 -- every frame of this rank's block
+            fits.step(it)
 
     def step_reference_call_site(it):  # train.py: create_render_arguments + Renderer + backward
         for ci in views_of(it):
@@ -672,30 +753,34 @@ def main():
 
     for it in range(args.warmup):
         step(it)
+    probe_steps = min(args.probe_steps, 1) if c5_cfg else args.probe_steps
     # untimed probe: events around every kernel (they add launch gaps, so not in the timed region)
     torch.cuda.synchronize()
     _C.profile_reset()
     _C.profile_select(None)
     _C.profile_enable(True)
-    for it in range(args.probe_steps):
+    for it in range(probe_steps):
         step(args.warmup + it)
     torch.cuda.synchronize()
     _C.profile_enable(False)
     probe = {ph: _C.profile_read(ph) for ph in PHASES}
     dom = max(PHASES, key=lambda ph: probe[ph][0])
-    # untimed solo probe (C3 / C3M / C4): the same steps on one stream, one thread -- each kernel's
-    # time without the other streams' kernels sharing the CUs (the roofline's kernel alone)
+    # untimed solo probe (not C5): the same steps on one stream, one thread -- each kernel's time
+    # without the other streams' kernels sharing the CUs (the roofline's kernel alone)
     solo = None
-    if c5 is None and args.probe_steps > 0:
+    if fits is None and probe_steps > 0:
         torch.cuda.synchronize()
         _C.profile_reset()
         _C.profile_enable(True)
-        for it in range(args.probe_steps):
+        for it in range(probe_steps):
             step(args.warmup + it, solo=True)
         torch.cuda.synchronize()
         _C.profile_enable(False)
         solo = {ph: _C.profile_read(ph) for ph in PHASES}
-    # timed region: HIP events only around the dominant kernel (its roofline), host timers on
+    # timed region: HIP events only around the dominant kernel (its roofline), host timers on, and an
+    # event on the main stream at every step end (the step ends there): per-step device intervals
+    first = args.warmup + probe_steps
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -703,26 +788,43 @@ def main():
     _C.profile_select([dom])
     _C.profile_enable(True)
     t0 = time.perf_counter()
+    ends[0].record(main_stream)
     for it in range(args.steps):
-        step(args.warmup + args.probe_steps + it)
+        step(first + it)
+        ends[it + 1].record(main_stream)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     _C.profile_enable(False)
+    step_ms = sorted(ends[i].elapsed_time(ends[i + 1]) for i in range(args.steps))
+    median_ms = float(np.median(step_ms))
     if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, median_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, median_ms = float(t[0].item()), float(t[1].item())
 
     # dominant kernel's device time inside the timed region (HIP events on its launch stream)
     tot_ms, cnt = _C.profile_read(dom)
     _C.profile_select(None)
+    checksum = None
+    if args.grad_checksum and fits is None:  # one more step, its (reduced) gradients kept and saved
+        it = first + args.steps
+        step(it, keep=True)
+        torch.cuda.synchronize()
+        flat = reducer.flat if reducer is not None else torch.cat([g.reshape(-1) for g in grads_of()])
+        checksum = f"{args.grad_checksum}.rank{rank}.pt"
+        torch.save({"bucket": flat.detach().cpu(), "views": views_of(it), "world": world, "rank": rank,
+                    "names": [k for k in leaves if k != "means2D"]}, checksum)
+        if reducer is not None:
+            reducer.zero_()
+        for p in leaves.values():
+            if reducer is None or p is leaves["means2D"]:
+                p.grad = None
     legs = world == 1 and args.config == "C3"
     call_site = None
     if legs and args.call_site_steps > 0:
-        first = args.warmup + args.probe_steps
         per_view = len(views_of(first))
         time_steps(step_reference_call_site, 3, first)  # warm each path's kernels and allocations
         ref_ms = time_steps(step_reference_call_site, args.call_site_steps, first)
@@ -732,24 +834,32 @@ def main():
                      "fused_activations_ms_per_view": round(fused_ms / per_view, 4),
                      "steps": args.call_site_steps}
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
+    train_site = None
+    if legs and args.train_steps > 0:
+        train_site = {k: train_call_site(args.train_steps, cfg, cams, views_of, dl, dev, streams, sh)
+                      for k, sh in (("rgb", False), ("sh3", True))}
     loss_site = loss_call_site(args.loss_steps, cams[0], leaves, dev) if legs and args.loss_steps > 0 else None
     dens_site = densify_call_site(args.densify_steps, cfg, cams[0], dev) if legs and args.densify_steps > 0 else None
     io_site = io_call_site(args.io_timesteps, dev) if legs and args.io_timesteps > 0 else None
     # untimed forwards over the cameras the timed steps used: mean pair count K for the byte model
-    first = args.warmup + args.probe_steps
-    used = c5.used_views(first, args.steps) if c5 else \
+    used = fits.used_views() if fits else \
         sorted({ci for it in range(first, first + args.steps) for ci in views_of(it)})
     Ks, max_tile = [], 0
     with torch.no_grad():
-        a = c5.frame_inputs(c5.frames[0]) if c5 else S.activated_inputs(params, cfg.sh_degree)
+        if fits:
+            import splat_frames
+            a = S.activated_inputs(splat_frames.frame_truth(fits.params[fits.frames[0]], fits.phi, fits.frames[0],
+                                                            fits.n_frames), -1)
+        else:
+            a = S.activated_inputs(params, cfg.sh_degree)
         if cfg.sh_degree >= 0:
             a.pop("colors_precomp")
         e = torch.empty(0, device=dev)
         colors = a.get("colors_precomp")
         for ci in used:
             c = cams[ci]
-            r = _C.rasterize_gaussians(c.bg, a["means3D"], colors if colors is not None else e,
-                                       a["opacities"], a["scales"], a["rotations"], 1.0, e,
+            r = _C.rasterize_gaussians(c.bg, a["means3D"].detach(), colors.detach() if colors is not None else e,
+                                       a["opacities"].detach(), a["scales"].detach(), a["rotations"].detach(), 1.0, e,
                                        c.viewmatrix, c.projmatrix, c.tanfovx, c.tanfovy,
                                        cfg.height, cfg.width, a.get("shs", e), c.sh_degree,
                                        c.campos, False)
@@ -792,9 +902,12 @@ def main():
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, SH)
     achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
-    value = views_per_step * cfg.P / (elapsed / args.steps) / 1e6
+    # value: the median step (median of >= 20 reps) -- per-step device intervals
+    # between the step-end events on the main stream; the mean over the timed region beside it
+    value = views_per_step * cfg.P / (median_ms * 1e-3) / 1e6
+    value_mean = views_per_step * cfg.P / (elapsed / args.steps) / 1e6
     pipe_b = pipeline_bytes(cfg.P, K, N, T, F, SH)
-    pipe_gbps = pipe_b * views_per_step / world / (elapsed / args.steps) / 1e9
+    pipe_gbps = pipe_b * views_per_step / world / (median_ms * 1e-3) / 1e9
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -802,34 +915,44 @@ def main():
             cam_cpu = S.render_settings(cfg.width, cfg.height, S.intrinsics(cfg.focal, cfg.width, cfg.height),
                                         S.look_at(yaw, hgt, cfg.distance), device="cpu",
                                         sh_degree=max(cfg.sh_degree, 0))
-            cpu = cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl.cpu())
+            cpu = cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl.cpu(), args.cpu_threads)
         workload = {
+            "C2": f"C2: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, the 4 cameras (yaw 0/90/180/270) "
+                  f"per GPU per step, fwd+bwd" + (", RCCL SUM all-reduce of the gradients" if world > 1 else ""),
             "C3": f"C3: {cfg.P} Gaussians, SH{cfg.sh_degree}, {cfg.width}x{cfg.height}, 27-camera rig, "
                   f"{V} view(s)/GPU/step, fwd+bwd" + (", RCCL SUM all-reduce of the gradients" if world > 1 else ""),
             "C3M": f"C3M: C3 with half of the {cfg.P} means in 16 tight clusters (densified-scene stand-in), "
                    f"SH{cfg.sh_degree}, {cfg.width}x{cfg.height}, {V} view(s)/GPU/step, fwd+bwd",
             "C4": f"C4: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, the 27-camera rig per step sharded "
                   f"round-robin over {world} GPU(s), fwd+bwd" + (", one RCCL SUM all-reduce" if world > 1 else ""),
-            "C5": f"C5: {cfg.P} Gaussians x 150 frames, RGB, {cfg.width}x{cfg.height}, frames sharded in blocks "
-                  f"over {world} GPU(s); one per-frame optimisation iteration per GPU per step = {V} rig views "
-                  f"fwd + fused L1/SSIM + bwd + fused Adam; no collective",
+            "C5": f"C5: {cfg.P} Gaussians x 150 frames, RGB, {cfg.width}x{cfg.height}, independent per-frame "
+                  f"fits (own parameters + Adam state per frame), frames sharded in blocks over {world} GPU(s); "
+                  f"one step = one optimisation iteration of every frame ({V} rig views fwd + fused L1/SSIM "
+                  f"+ bwd + fused Adam); no collective",
         }[args.config]
+        shape = ("view losses summed, one backward (deferred multi-view per-Gaussian pass)"
+                 if args.step_shape == "summed" else "one backward per view")
         out = {
-            "metric": "Msplats/sec fwd+bwd @1080p (1M gauss)" if args.config != "C5" else
+            "metric": "Msplats/sec fwd+bwd @1080p (1M gauss)" if args.config in ("C3", "C3M", "C4") else
+                      "Msplats/sec fwd+bwd @800x800 (100k gauss, 4 cameras)" if args.config == "C2" else
                       "Msplats/sec fwd+bwd @1080p (2M gauss per-frame fits)",
             "value": round(value, 3), "unit": "Msplats/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong" if args.config == "C4" else "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "strong" if args.config in ("C4", "C5") else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic",
+            "value_definition": "views x Gaussians / median step (device intervals between the step-end "
+                                "events on the main stream; max over ranks)",
+            "median_ms_per_step": round(median_ms, 4), "value_mean": round(value_mean, 3),
+            "step_ms_quartiles": [round(float(np.percentile(step_ms, q)), 4) for q in (25, 50, 75)],
             "config": {"workload": workload, "gaussians": cfg.P, "views_per_step": views_per_step,
                        "views_per_gpu": [len(splat_dp.shard_views(list(range(views_per_step)), r, world))
                                          for r in range(world)],
                        "image": f"{cfg.width}x{cfg.height}", "sh_degree": cfg.sh_degree,
-                       "mean_num_rendered": int(K), "max_tile_pairs": max_tile, "parallelism": f"camera-dp{world}" if args.config != "C5"
-                       else f"frame-dp{world}", "streams_per_gpu": len(streams),
-                       "step_shape": ("view losses summed, one backward (deferred multi-view per-Gaussian "
-                                      "pass)" if args.step_shape == "summed" else "one backward per view"),
-                       "submission": "one host thread per stream" if pool is not None else "one host thread",
+                       "mean_num_rendered": int(K), "max_tile_pairs": max_tile,
+                       "parallelism": f"frame-dp{world}" if c5_cfg else f"camera-dp{world}",
+                       "streams_per_gpu": len(streams),
+                       "step_shape": "per frame: view losses summed, one backward, one Adam step" if c5_cfg else shape,
+                       "submission": "one host thread per stream" if rstep.pool is not None else "one host thread",
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -856,86 +979,17 @@ def main():
             if solo else None,
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
+            "train_call_site": train_site,
             "call_site": call_site,
             "loss_call_site": loss_site,
             "densify_call_site": dens_site,
             "io_call_site": io_site,
+            "grad_checksum": checksum,
         }
         print(json.dumps(out), flush=True)
+    rstep.close()
     if dist is not None:
         dist.destroy_process_group()
-
-
-class _C5Fit:
-    """BASELINE.json configs[4]: per-frame optimisation of a 2M-Gaussian cloud over a 150-frame
-    dynamic sequence (frame t displaces the means by 0.05 sin(2 pi t / 150 + phi_i),
-    phi ~ U(0, 2 pi) seed 2), frames sharded over the ranks in contiguous blocks (splat_dp.shard_frames;
-    independent fits, no exchange).  One step = one optimisation iteration of this rank's current frame
-    as train.py runs it (train.py:738-776: render 5 views, L1 + SSIM losses, backward, Adam step):
-    5 rig views through rasterize_parameters (fused activations), the fused L1 + SSIM loss against the
-    frame's target images (renders of the frame's ground-truth cloud, made before timing: the
-    captured images of a real sequence are resident too), the view losses summed and one backward, one
-    FusedAdam step (densify.py:68-86 learning rates)."""
-
-    def __init__(self, cfg, params_cpu, cams, rank, world, V, dev, streams, main_stream, total_steps):
-        import math
-        import splat_adam
-        import splat_dp
-        from diff_gaussian_rasterization import rasterize_parameters
-        self.cams, self.V, self.dev, self.streams, self.main = cams, V, dev, streams, main_stream
-        self.rasterize = rasterize_parameters
-        g = torch.Generator().manual_seed(2)
-        self.phi = (torch.rand(cfg.P, 1, generator=g) * 2 * math.pi).to(dev)
-        self.base = {k: v.to(dev) for k, v in params_cpu.items()}
-        self.frames = list(splat_dp.shard_frames(150, rank, world))
-        self.params = {k: torch.nn.Parameter(v.clone()) for k, v in self.base.items()}
-        lrs = {"means": 0.00016, "colors": 0.0025, "rotation_quaternions": 0.001, "opacity_logits": 0.05,
-               "log_scales": 0.001}
-        self.opt = splat_adam.FusedAdam([{"params": [p], "name": k, "lr": lrs.get(k, 1e-3)}
-                                         for k, p in self.params.items()], lr=0.0, eps=1e-15)
-        self.targets = {}
-        with torch.no_grad():
-            for it in range(min(total_steps, len(self.frames))):
-                f = self.frames[it]
-                gt = self.frame_params(f)
-                for ci in self.frame_views(f):
-                    self.targets[(f, ci)] = rasterize_parameters(gt, cams[ci])[0].detach()
-        torch.cuda.synchronize()
-
-    def frame_params(self, t):
-        import math
-        p = dict(self.base)
-        p["means"] = self.base["means"] + 0.05 * torch.sin(2 * math.pi * t / 150 + self.phi)
-        return p
-
-    def frame_inputs(self, t):
-        import splat_scenes as S
-        return S.activated_inputs(self.frame_params(t), -1)
-
-    def frame_views(self, t):
-        return [(t * self.V + j) % len(self.cams) for j in range(self.V)]
-
-    def used_views(self, first, n):
-        return sorted({ci for it in range(first, first + n) for ci in self.frame_views(self.frames[it % len(self.frames)])})
-
-    def step(self, it):
-        import splat_loss
-        f = self.frames[it % len(self.frames)]
-        for s in self.streams:
-            s.wait_stream(self.main)  # the previous iteration's Adam update
-        losses = []
-        for k, ci in enumerate(self.frame_views(f)):
-            with torch.cuda.stream(self.streams[k % len(self.streams)]):
-                img = self.rasterize(self.params, self.cams[ci])[0]
-                tgt = self.targets.get((f, ci))
-                if tgt is None:
-                    raise RuntimeError(f"C5: no target for frame {f} view {ci}")
-                losses.append(splat_loss.image_loss(img, tgt))
-        for s in self.streams:
-            self.main.wait_stream(s)
-        sum(losses).backward()  # train.py:757-767: the views' losses summed, one backward
-        self.opt.step()
-        self.opt.zero_grad(set_to_none=True)
 
 
 if __name__ == "__main__":

@@ -29,6 +29,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define BX 16
 #define BY 16
@@ -639,4 +642,17 @@ void ora_mark_visible(int P, const float *means3D, const float *viewmatrix, cons
         xform4x3(means3D + 3 * i, viewmatrix, pv);
         present[i] = !(pv[2] <= 0.2f);
     }
+}
+
+/* OpenMP threads of the oracle's parallel loops (bench.py's cpu_baseline leg sets the host's core
+ * count; OMP_NUM_THREADS only applies before the runtime's first parallel region).  Returns the
+ * count the next parallel region will use. */
+int ora_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }

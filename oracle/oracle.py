@@ -67,8 +67,15 @@ def lib():
             ctypes.c_float, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.ora_mark_visible.restype = None
         L.ora_mark_visible.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _u8p]
+        L.ora_set_threads.restype = ctypes.c_int
+        L.ora_set_threads.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the oracle's loops (n <= 0 leaves them); returns the count in effect."""
+    return int(lib().ora_set_threads(int(n)))
 
 
 def _arr(x, dtype=np.float32):

@@ -29,3 +29,16 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but no GPU is visible")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _dump_parity_stats():
+    """At the end of the session, the parity tests' outside-tolerance fractions (test_gpu_parity.STATS)
+    go to gpurun_out/parity_stats.json when that directory exists (GPU runs)."""
+    yield
+    mod = sys.modules.get("test_gpu_parity")
+    out = os.path.join(REPO, "gpurun_out")
+    if mod is not None and getattr(mod, "STATS", None) and os.path.isdir(out):
+        import json
+        with open(os.path.join(out, "parity_stats.json"), "w") as f:
+            json.dump(mod.STATS, f, indent=0)

@@ -6,7 +6,8 @@ depth and every gradient within 1e-4 relative (fp32).  Gradients are summed in a
 than the oracle (per-tile wave reductions vs. a serial loop), so they are compared with
 |gpu - oracle| <= 1e-4 |oracle| + 1e-5 max|oracle|.  Blend decisions (alpha >= 1/255,
 T >= 1e-4) can flip when GPU expf and glibc expf differ by an ulp on a pair sitting exactly on a
-threshold; that is allowed for at most 1e-4 of the pixels and reported.
+threshold; such values are allowed per case at 4x the rate measured on the box (ALLOW) and
+reported in gpurun_out/parity_stats.json.
 """
 import os
 
@@ -21,18 +22,22 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-4
-STATS = []  # (test, quantity, mismatch fraction, worst abs err, scale) -> gpurun_out/parity_stats.json
+# Per-case allowances for values outside tolerance (pixels, gradient values): 4x the rates measured on
+# the box (profiles/r02_parity_flips.json; cases that measured 0 allow 0).  The flips are blend
+# decisions (alpha >= 1/255, T >= 1e-4) that a few-ulp exp difference moves across a threshold.
+ALLOW = {
+    "c1": (6.1e-5, 1.07e-3),
+    "C2_yaw0": (6.3e-6, 4e-5), "C2_yaw180": (1.25e-5, 2e-4),
+    "C3_yaw0": (9.6e-6, 3.6e-5),
+    "C4_yaw40_up": (5.8e-6, 2e-5), "C4_yaw200_down": (1.9e-6, 4e-5),
+}
 
 
-@pytest.fixture(autouse=True, scope="module")
-def _dump_stats():
-    yield
-    import json
-    import os
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
-    if os.path.isdir(out):
-        with open(os.path.join(out, "parity_stats.json"), "w") as f:
-            json.dump(STATS, f, indent=0)
+def allow(case):
+    return ALLOW.get(case, (0.0, 0.0))
+# (test, quantity, mismatch fraction, worst abs err, scale, fraction at a 1e-6 floor) -> gpurun_out/parity_stats.json
+# (dumped by conftest.py at the end of the session; test_headline_parity.py appends to it too)
+STATS = []
 
 
 def _inputs(P, W, H, focal, s0, seed=0, sh_degree=-1, yaw=0.0, height=0.0, distance=4.0,
@@ -98,15 +103,17 @@ def _close(name, got, ref, rtol=RTOL, atol_frac=1e-5, max_bad_frac=0.0):
     if ref.size == 0:
         return
     scale = np.abs(ref).max() + 1e-30
-    bad = np.abs(got - ref) > rtol * np.abs(ref) + atol_frac * scale
+    err = np.abs(got - ref)
+    bad = err > rtol * np.abs(ref) + atol_frac * scale
     frac = bad.mean()
+    tight = float((err > rtol * np.abs(ref) + 1e-6 * scale).mean())  # informational: a 10x lower floor
     STATS.append((os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], name, float(frac),
-                  float(np.abs(got - ref).max()), float(scale)))
+                  float(err.max()), float(scale), tight))
     assert frac <= max_bad_frac, (f"{name}: {bad.sum()}/{bad.size} outside tolerance, worst "
                                   f"{np.abs(got - ref).max():.3g} (scale {scale:.3g})")
 
 
-def check_forward(fw, st, pix_flip_frac=1e-4):
+def check_forward(fw, st, pix_flip_frac=0.0):
     """Bit-exact integer state + tolerance on blended images."""
     d = fw["dec"]
     P = st["P"]
@@ -149,7 +156,7 @@ def check_forward(fw, st, pix_flip_frac=1e-4):
     assert fw["color"].shape == (3, H, W) and fw["depth"].shape == (1, H, W)
 
 
-def check_backward(gb, gref, P, M, grad_flip_frac=1e-3):
+def check_backward(gb, gref, P, M, grad_flip_frac=0.0):
     (dm2, dcol, dop, dm3, dcov, dsh, dsc, drot) = [_np(t) for t in gb]
     _close("means2D", dm2, gref["means2D"], max_bad_frac=grad_flip_frac)
     _close("colors", dcol, gref["colors"], max_bad_frac=grad_flip_frac)
@@ -183,11 +190,12 @@ def test_forward_backward_parity(case, cuda):
     a, rs = _inputs(P, W, H, f, s0, seed=3, sh_degree=shd, **extra)
     st = _ora_forward(a, rs)
     fw = _gpu_forward(a, rs, cuda)
-    check_forward(fw, st)
+    pix, grad = allow(case)
+    check_forward(fw, st, pix)
     dl = S.upstream_grad(H, W, device="cpu")
     gref = O.backward(st, dl.numpy())
     gb = _gpu_backward(a, rs, cuda, fw, dl)
-    check_backward(gb, gref, P, st["M"])
+    check_backward(gb, gref, P, st["M"], grad)
 
 
 def test_cov3d_precomp_parity(cuda):
@@ -286,8 +294,8 @@ def test_rasterizer_module_autograd(cuda):
                                      projmatrix=rs.projmatrix.cpu(), campos=rs.campos.cpu()))
     np.testing.assert_array_equal(_np(radii), st["radii"])
     gref = O.backward(st, dl.cpu().numpy())
-    _close("means2D.grad", _np(args["means2D"].grad), gref["means2D"], max_bad_frac=1e-3)
-    _close("colors.grad", _np(params["colors"].grad), gref["colors"], max_bad_frac=1e-3)
+    _close("means2D.grad", _np(args["means2D"].grad), gref["means2D"], max_bad_frac=0.0)
+    _close("colors.grad", _np(params["colors"].grad), gref["colors"], max_bad_frac=0.0)
     assert params["means"].grad is not None and params["log_scales"].grad is not None
     assert params["rotation_quaternions"].grad is not None and params["opacity_logits"].grad is not None
     with pytest.raises(Exception):
@@ -332,19 +340,20 @@ def test_fused_parameters_parity(case, cuda):
                                                shs=gp["shs"] if shd >= 0 else None)
     (color * dl.to(cuda)).sum().backward()
     same_r = (_np(radii) == st["radii"]).mean()
+    STATS.append((f"test_fused_parameters_parity[{case}]", "radii", float(1 - same_r), 0.0, 0.0))
     assert same_r >= 1 - 1e-3, f"radii differ on {1 - same_r:.2e} of Gaussians"
-    _close("fused.color", _np(color), st["color"], atol_frac=1e-6, max_bad_frac=1e-4)
-    _close("fused.depth", _np(depth), st["depth"], atol_frac=1e-6, max_bad_frac=1e-4)
-    _close("fused.means2D", _np(means2D.grad), gref["means2D"], max_bad_frac=1e-3)
-    _close("fused.means", _np(gp["means"].grad), gref["means3D"], max_bad_frac=1e-3)
+    _close("fused.color", _np(color), st["color"], atol_frac=1e-6, max_bad_frac=0.0)
+    _close("fused.depth", _np(depth), st["depth"], atol_frac=1e-6, max_bad_frac=0.0)
+    _close("fused.means2D", _np(means2D.grad), gref["means2D"], max_bad_frac=0.0)
+    _close("fused.means", _np(gp["means"].grad), gref["means3D"], max_bad_frac=0.0)
     if shd >= 0:
-        _close("fused.shs", _np(gp["shs"].grad), gref["sh"], max_bad_frac=1e-3)
+        _close("fused.shs", _np(gp["shs"].grad), gref["sh"], max_bad_frac=0.0)
         assert gp["colors"].grad is None
     else:
-        _close("fused.colors", _np(gp["colors"].grad), gref["colors"], max_bad_frac=1e-3)
+        _close("fused.colors", _np(gp["colors"].grad), gref["colors"], max_bad_frac=0.0)
     for k in ("opacity_logits", "log_scales", "rotation_quaternions"):
         assert gp[k].grad.shape == raw[k].shape
-        _close("fused." + k, _np(gp[k].grad), raw[k].grad.numpy(), max_bad_frac=1e-3)
+        _close("fused." + k, _np(gp[k].grad), raw[k].grad.numpy(), max_bad_frac=0.0)
 
 
 def test_strided_camera_inputs_match_contiguous(cuda):
@@ -404,16 +413,17 @@ def _baseline_cloud(name):
 def test_baseline_size_parity(view, cuda):
     """C2 / C3 / C4 at the BASELINE.json sizes against the C oracle: bit-exact radii, rects, tiles,
     K, point lists, ranges, emission offsets; colour / depth / every gradient within 1e-4 rel with
-    the same blend-flip allowances as the small cases (flip rates recorded in parity_stats.json)."""
+    per-view blend-flip allowances of 4x the measured rates (ALLOW; rates in parity_stats.json)."""
     name, yaw, hgt = BASELINE_VIEWS[view]
     cfg, a = _baseline_cloud(name)
     rs = S.render_settings(cfg.width, cfg.height, S.intrinsics(cfg.focal, cfg.width, cfg.height),
                            S.look_at(yaw, hgt, cfg.distance), device="cpu", sh_degree=max(cfg.sh_degree, 0))
     st = _ora_forward(a, rs)
     fw = _gpu_forward(a, rs, cuda)
-    check_forward(fw, st)
+    pix, grad = allow(view)
+    check_forward(fw, st, pix)
     dl = S.upstream_grad(cfg.height, cfg.width, device="cpu")
     gref = O.backward(st, dl.numpy())
     gb = _gpu_backward(a, rs, cuda, fw, dl)
-    check_backward(gb, gref, cfg.P, st["M"])
+    check_backward(gb, gref, cfg.P, st["M"], grad)
     STATS.append((view, "num_rendered", float(st["num_rendered"]), 0.0, 0.0))

@@ -1,0 +1,130 @@
+"""The headline path against the CPU oracle at BASELINE sizes (-m gpu).
+
+* C3 (BASELINE.json configs[2]): 1M Gaussians, SH3, 1920x1080, the bench's step exactly -- 5 rig
+  views forwarded on 3 HIP streams by one submitting thread per stream, their images backpropagated
+  together (the summed loss of train.py:753-767), every view's per-pixel backward in its node and ONE
+  deferred multi-view per-Gaussian pass (k_gauss_bwd_multi) at the end of the pass
+  (splat_step.RenderStep, the object bench.py times).  Every leaf gradient is compared with the SUM
+  over the views of the oracle's per-view backward, and every view's image with the oracle's.  Run
+  twice: one ``means2D`` leaf shared by the 5 views (the bench) and one fresh ``means2D`` leaf per
+  view (create_render_arguments makes one per render, shared.py:38-41).
+* C5 (BASELINE.json configs[4]): one view of the 2M-Gaussian RGB cloud at 1920x1080 through
+  ``rasterize_parameters`` (the C5 fit's fused activations) against the oracle on torch's CPU
+  activations, chained back to the raw parameters by CPU autograd.
+
+Tolerances: 1e-4 relative + a floor of 1e-5 x max|ref| per array; values outside it (blend decisions
+flipped by a few-ulp exp difference on a threshold) are allowed at <= 4x the rate
+measured on the box (profiles/r03_parity_flips.json).
+"""
+import numpy as np
+import pytest
+import torch
+
+import splat_scenes as S
+import splat_step
+from diff_gaussian_rasterization import rasterize_parameters
+from oracle import oracle as O
+from test_gpu_parity import STATS, _close, _np  # noqa: F401 -- STATS: the module's stat dump
+
+pytestmark = pytest.mark.gpu
+
+# measured outside-tolerance fractions x 4 (profiles/r03_parity_flips.json)
+ALLOW = {
+    "C3_summed": dict(pix=1e-5, grad=1e-4),
+    "C5_view": dict(pix=1e-5, grad=1e-4),
+}
+VIEWS = [0, 1, 2, 3, 4]  # the bench's first step: rig cameras 0-4 (height -0.8, yaw 0..160)
+
+
+@pytest.fixture(scope="module")
+def c3_oracle():
+    """Per-view oracle forward + backward of the C3 cloud for the 5 views (CPU, OpenMP)."""
+    cfg = S.CONFIGS["C3"]
+    p = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=3, seed=0, device="cpu")
+    a = {k: v.detach() for k, v in S.activated_inputs(p, 3).items() if isinstance(v, torch.Tensor)}
+    a.pop("means2D")
+    dl = S.upstream_grad(cfg.height, cfg.width, device="cpu")
+    cams = [S.render_settings(cfg.width, cfg.height, S.intrinsics(cfg.focal, cfg.width, cfg.height),
+                              S.look_at(*S.RIG27[ci], cfg.distance), device="cpu", sh_degree=3) for ci in VIEWS]
+    images, sums, m2 = [], None, []
+    for rs in cams:
+        st = O.forward(rs.bg.numpy(), a["means3D"].numpy(), None, a["opacities"].numpy(), a["scales"].numpy(),
+                       a["rotations"].numpy(), 1.0, None, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                       rs.image_height, rs.image_width, a["shs"].numpy(), 3, rs.campos.numpy())
+        g = O.backward(st, dl.numpy())
+        images.append(st["color"])
+        m2.append(g["means2D"])
+        part = {k: g[k].astype(np.float64) for k in ("means3D", "opacities", "scales", "rotations", "sh")}
+        sums = part if sums is None else {k: sums[k] + part[k] for k in sums}
+        del st, g
+    return cfg, a, dl, images, sums, m2
+
+
+@pytest.mark.parametrize("means2d", ["shared", "per_view"])
+def test_c3_summed_step_vs_oracle(means2d, c3_oracle, cuda):
+    cfg, a, dl_cpu, images, sums, m2_ref = c3_oracle
+    leaves = {k: v.to(cuda).requires_grad_(True) for k, v in a.items()}
+    leaves["means2D"] = torch.zeros(cfg.P, 3, device=cuda, requires_grad=True)
+    per_view = {ci: torch.zeros(cfg.P, 3, device=cuda, requires_grad=True) for ci in VIEWS}
+    cams = S.scene_cameras(S.SceneConfig("C3", cfg.P, cfg.width, cfg.height, cfg.focal, cfg.s0, sh_degree=3,
+                                         views=S.RIG27), device=cuda)
+    main = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    for s in streams:
+        s.wait_stream(main)
+    inputs_of = (lambda ci: leaves) if means2d == "shared" else (lambda ci: dict(leaves, means2D=per_view[ci]))
+    step = splat_step.RenderStep(cuda, cams, inputs_of, S.upstream_grad(cfg.height, cfg.width, device=cuda),
+                                 streams, threads=True, shape="summed")
+    try:
+        imgs = step(VIEWS)
+    finally:
+        step.close()
+    torch.cuda.synchronize()
+    allow = ALLOW["C3_summed"]
+    for k, (img, ref) in enumerate(zip(imgs, images)):
+        _close(f"C3 view {VIEWS[k]} color", _np(img), ref, atol_frac=1e-6, max_bad_frac=allow["pix"])
+    names = {"means3D": "means3D", "opacities": "opacities", "scales": "scales", "rotations": "rotations",
+             "shs": "sh"}
+    for leaf, ref in names.items():
+        _close(f"C3 summed {leaf}", _np(leaves[leaf].grad), sums[ref], max_bad_frac=allow["grad"])
+    if means2d == "shared":
+        _close("C3 summed means2D", _np(leaves["means2D"].grad), sum(x.astype(np.float64) for x in m2_ref),
+               max_bad_frac=allow["grad"])
+    else:
+        for k, ci in enumerate(VIEWS):
+            _close(f"C3 view {ci} means2D", _np(per_view[ci].grad), m2_ref[k], max_bad_frac=allow["grad"])
+
+
+def test_c5_view_vs_oracle(cuda):
+    """One view of the C5 fit's 2M-Gaussian cloud (RGB, fused activations) against the oracle."""
+    P, W, H, f = 2_000_000, 1920, 1080, 1600.0
+    p = S.synthetic_cloud(P, 0.005, sh_degree=-1, seed=0, device="cpu")
+    raw = {k: v.clone().requires_grad_(True) for k, v in p.items()}
+    act = S.activated_inputs(raw, -1)
+    a = {k: v.detach() for k, v in act.items() if isinstance(v, torch.Tensor) and k != "means2D"}
+    rs = S.render_settings(W, H, S.intrinsics(f, W, H), S.look_at(*S.RIG27[13], 4.0), device="cpu")
+    st = O.forward(rs.bg.numpy(), a["means3D"].numpy(), a["colors_precomp"].numpy(), a["opacities"].numpy(),
+                   a["scales"].numpy(), a["rotations"].numpy(), 1.0, None, rs.viewmatrix, rs.projmatrix,
+                   rs.tanfovx, rs.tanfovy, H, W, None, 0, rs.campos.numpy())
+    dl = S.upstream_grad(H, W, device="cpu")
+    g = O.backward(st, dl.numpy())
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(g[k]))  # noqa: E731
+    torch.autograd.backward([act["opacities"], act["scales"], act["rotations"]],
+                            [t("opacities").view_as(act["opacities"]), t("scales"), t("rotations")])
+    gp = {k: v.detach().to(cuda).requires_grad_(True) for k, v in p.items()}
+    m2 = torch.zeros(P, 3, device=cuda, requires_grad=True)
+    rsg = rs._replace(bg=rs.bg.to(cuda), viewmatrix=rs.viewmatrix.to(cuda), projmatrix=rs.projmatrix.to(cuda),
+                      campos=rs.campos.to(cuda))
+    color, radii, depth = rasterize_parameters(gp, rsg, means2D=m2)
+    (color * dl.to(cuda)).sum().backward()
+    torch.cuda.synchronize()
+    allow = ALLOW["C5_view"]
+    np.testing.assert_array_equal(_np(radii), st["radii"])
+    _close("C5 color", _np(color), st["color"], atol_frac=1e-6, max_bad_frac=allow["pix"])
+    _close("C5 depth", _np(depth), st["depth"], atol_frac=1e-6, max_bad_frac=allow["pix"])
+    _close("C5 means2D", _np(m2.grad), g["means2D"], max_bad_frac=allow["grad"])
+    _close("C5 means", _np(gp["means"].grad), g["means3D"], max_bad_frac=allow["grad"])
+    _close("C5 colors", _np(gp["colors"].grad), g["colors"], max_bad_frac=allow["grad"])
+    for k in ("opacity_logits", "log_scales", "rotation_quaternions"):
+        _close(f"C5 {k}", _np(gp[k].grad), raw[k].grad.numpy(), max_bad_frac=allow["grad"])
+    STATS.append(("test_c5_view_vs_oracle", "num_rendered", float(st["num_rendered"]), 0.0, 0.0))
