@@ -402,8 +402,6 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     if (rc) return rc;
     if (!out) return fail(GSR_ERR_ARG, "gsr_backward: null grads");
     if (g->P == 0) return GSR_OK;
-    if (!out->dL_dmeans2D || !out->dL_dopacity || !out->dL_dmeans3D || (g->shs && !out->dL_dsh))
-        return fail(GSR_ERR_ARG, "gsr_backward: missing gradient output");
     if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward: unknown accumulate bits 0x%x", out->accumulate);
     hipStream_t s = (hipStream_t)stream;
     BwdArgs a;
@@ -443,8 +441,6 @@ int gsr_backward_gaussians(int nviews, const gsr_view_grad *views, const gsr_gau
     if (g->P == 0) return GSR_OK;
     if (g->shs && g->sh_coeffs != 1 && g->sh_coeffs != 4 && g->sh_coeffs != 9 && g->sh_coeffs != 16)
         return fail(GSR_ERR_UNSUPPORTED, "gsr_backward_gaussians: %d SH coefficients (1, 4, 9 or 16 supported)", g->sh_coeffs);
-    if (!out->dL_dopacity || !out->dL_dmeans3D || (g->shs && !out->dL_dsh))
-        return fail(GSR_ERR_ARG, "gsr_backward_gaussians: missing gradient output");
     if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward_gaussians: unknown accumulate bits 0x%x", out->accumulate);
     for (int v = 0; v < nviews; ++v)
         if (!views[v].radii || !views[v].geom || !views[v].scratch || views[v].num_rendered < 0)

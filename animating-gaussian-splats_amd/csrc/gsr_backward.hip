@@ -475,18 +475,20 @@ __device__ inline float3 sh_backward(int deg, int M, float3 mean, float3 campos,
     float basis[16];
     sh_basis16(x, y, z, basis);
     const int active = (deg + 1) * (deg + 1);
+    if (dL_dsh) {  // null: the coefficients' gradient is not requested (only the mean's)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if (i < M) {
+        for (int i = 0; i < 16; ++i) {
+            if (i < M) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float v = i < active ? basis[i] * dRGB[c] : 0.f;
-                dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] + v : v;
+                for (int c = 0; c < 3; ++c) {
+                    const float v = i < active ? basis[i] * dRGB[c] : 0.f;
+                    dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] + v : v;
+                }
             }
         }
+        for (int i = 16; i < M; ++i)
+            for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] : 0.f;
     }
-    for (int i = 16; i < M; ++i)
-        for (int c = 0; c < 3; ++c) dL_dsh[i * 3 + c] = acc ? dL_dsh[i * 3 + c] : 0.f;
     return unit_vec_bwd(d0, dL_ddir);
 }
 
@@ -679,7 +681,7 @@ __device__ inline void gauss_bwd_one(
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec, int accm) {
-    // dL_dcolors / dL_dcov3D / dL_dscales / dL_drot may be NULL (gradient not requested); accm:
+    // every output may be NULL (gradient not requested: the input does not require grad); accm:
     // gsr_grad_bits of the outputs to add into instead of overwrite
     const bool a2 = accm & GSR_GRAD_MEANS2D, ac = accm & GSR_GRAD_COLORS, ao = accm & GSR_GRAD_OPACITY,
                a3 = accm & GSR_GRAD_MEANS3D, acv = accm & GSR_GRAD_COV3D, ash = accm & GSR_GRAD_SH,
@@ -687,12 +689,12 @@ __device__ inline void gauss_bwd_one(
     if (!(radii[i] > 0)) {  // zero gradient: accumulated outputs keep their content
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            if (!a2) dL_dmeans2D[3 * i + k] = 0.f;
-            if (!a3) dL_dmeans3D[3 * i + k] = 0.f;
+            if (dL_dmeans2D && !a2) dL_dmeans2D[3 * i + k] = 0.f;
+            if (dL_dmeans3D && !a3) dL_dmeans3D[3 * i + k] = 0.f;
             if (dL_dcolors && !ac) dL_dcolors[3 * i + k] = 0.f;
             if (dL_dscales && !asc) dL_dscales[3 * i + k] = 0.f;
         }
-        if (!ao) dL_dopacity[i] = 0.f;
+        if (dL_dopacity && !ao) dL_dopacity[i] = 0.f;
         if (dL_dcov3D && !acv) {
 #pragma unroll
             for (int k = 0; k < 6; ++k) dL_dcov3D[6 * i + k] = 0.f;
@@ -711,13 +713,16 @@ __device__ inline void gauss_bwd_one(
     }
     {   // screen-space outputs: old values (accumulation) fetched together
         float o2[3], oo[1], oc[3];
-        old_load(dL_dmeans2D, 3 * (size_t)i, a2, o2);
-        old_load(dL_dopacity, (size_t)i, ao, oo);
+        old_load(dL_dmeans2D, 3 * (size_t)i, dL_dmeans2D && a2, o2);
+        old_load(dL_dopacity, (size_t)i, dL_dopacity && ao, oo);
         old_load(dL_dcolors, 3 * (size_t)i, dL_dcolors && ac, oc);
-        gput_old(dL_dmeans2D, 3 * i, acc[0], a2, o2[0]); gput_old(dL_dmeans2D, 3 * i + 1, acc[1], a2, o2[1]);
-        gput_old(dL_dmeans2D, 3 * i + 2, 0.f, a2, o2[2]);
+        if (dL_dmeans2D) {
+            gput_old(dL_dmeans2D, 3 * i, acc[0], a2, o2[0]); gput_old(dL_dmeans2D, 3 * i + 1, acc[1], a2, o2[1]);
+            gput_old(dL_dmeans2D, 3 * i + 2, 0.f, a2, o2[2]);
+        }
         // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
-        if (act & GSR_ACT_SIGMOID_OPACITY) {
+        if (!dL_dopacity) {
+        } else if (act & GSR_ACT_SIGMOID_OPACITY) {
             const float o = rec[(size_t)kRecF4 * i + 1].y;
             gput_old(dL_dopacity, i, acc[5] * ((1.f - o) * o), ao, oo[0]);
         } else {
@@ -764,18 +769,20 @@ __device__ inline void gauss_bwd_one(
         const float3 cp = load_campos(campos, cs.c0);
         (void)sh_to_rgb(D, mean, cp, sh, cl);
         const float3 d = sh_backward(D, M, mean, cp, sh, cl, make_float3(acc[6], acc[7], acc[8]),
-                                     dL_dsh + (size_t)i * M * 3, ash);
+                                     dL_dsh ? dL_dsh + (size_t)i * M * 3 : nullptr, ash);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
     } else if (dL_dsh) {
         if (!ash) for (int k = 0; k < M * 3; ++k) dL_dsh[(size_t)i * M * 3 + k] = 0.f;
     }
     const bool has_sr = scales && !cov3D_precomp;
     float o3[3], os[3], orr[4];  // old values of the remaining accumulated outputs, fetched together
-    old_load(dL_dmeans3D, 3 * (size_t)i, a3, o3);
+    old_load(dL_dmeans3D, 3 * (size_t)i, dL_dmeans3D && a3, o3);
     old_load(dL_dscales, 3 * (size_t)i, has_sr && dL_dscales && asc, os);
     old_load(dL_drot, 4 * (size_t)i, has_sr && dL_drot && ar, orr);
-    gput_old(dL_dmeans3D, 3 * i, dm0, a3, o3[0]); gput_old(dL_dmeans3D, 3 * i + 1, dm1, a3, o3[1]);
-    gput_old(dL_dmeans3D, 3 * i + 2, dm2, a3, o3[2]);
+    if (dL_dmeans3D) {
+        gput_old(dL_dmeans3D, 3 * i, dm0, a3, o3[0]); gput_old(dL_dmeans3D, 3 * i + 1, dm1, a3, o3[1]);
+        gput_old(dL_dmeans3D, 3 * i + 2, dm2, a3, o3[2]);
+    }
     if (has_sr) {
         float3 ds; float4 dr;
         cov3d_backward(s3, scale_modifier, q, dcov, ds, dr);
@@ -826,6 +833,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
                                  act, rec, accm);
     if constexpr (MC > 0) {  // coalesced store of the dL/dSH rows
+        if (!dL_dsh) return;
         __syncthreads();
         if (accm & GSR_GRAD_SH) sh_rows_from_lds<MC, true>(s_sh, nrow, dL_dsh + (size_t)i0 * RL);
         else sh_rows_from_lds<MC, false>(s_sh, nrow, dL_dsh + (size_t)i0 * RL);
@@ -1024,11 +1032,11 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if (!vis) {  // no view sees it: zero gradient, accumulated outputs keep their content
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
-                if (!a3) a.dL_dmeans3D[3 * i + k] = 0.f;
+                if (a.dL_dmeans3D && !a3) a.dL_dmeans3D[3 * i + k] = 0.f;
                 if (a.dL_dcolors && !ac) a.dL_dcolors[3 * i + k] = 0.f;
                 if (a.dL_dscales && !asc) a.dL_dscales[3 * i + k] = 0.f;
             }
-            if (!ao) a.dL_dopacity[i] = 0.f;
+            if (a.dL_dopacity && !ao) a.dL_dopacity[i] = 0.f;
             if (a.dL_dcov3D && !acv) {
 #pragma unroll
                 for (int k = 0; k < 6; ++k) a.dL_dcov3D[6 * i + k] = 0.f;
@@ -1039,10 +1047,11 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             }
         } else {
             float oo[1], oc[3], o3[3];
-            old_load(a.dL_dopacity, (size_t)i, ao, oo);
+            old_load(a.dL_dopacity, (size_t)i, a.dL_dopacity && ao, oo);
             old_load(a.dL_dcolors, 3 * (size_t)i, a.dL_dcolors && ac, oc);
-            old_load(a.dL_dmeans3D, 3 * (size_t)i, a3, o3);
-            if (a.act & GSR_ACT_SIGMOID_OPACITY) {  // d/dlogit = o (1 - o), o from a forward's record
+            old_load(a.dL_dmeans3D, 3 * (size_t)i, a.dL_dmeans3D && a3, o3);
+            if (!a.dL_dopacity) {
+            } else if (a.act & GSR_ACT_SIGMOID_OPACITY) {  // d/dlogit = o (1 - o), o from a forward's record
                 gput_old(a.dL_dopacity, i, gop * ((1.f - o_act) * o_act), ao, oo[0]);
             } else {
                 gput_old(a.dL_dopacity, i, gop, ao, oo[0]);
@@ -1051,8 +1060,10 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
                 gput_old(a.dL_dcolors, 3 * i, gc0, ac, oc[0]); gput_old(a.dL_dcolors, 3 * i + 1, gc1, ac, oc[1]);
                 gput_old(a.dL_dcolors, 3 * i + 2, gc2, ac, oc[2]);
             }
-            gput_old(a.dL_dmeans3D, 3 * i, gm0, a3, o3[0]); gput_old(a.dL_dmeans3D, 3 * i + 1, gm1, a3, o3[1]);
-            gput_old(a.dL_dmeans3D, 3 * i + 2, gm2, a3, o3[2]);
+            if (a.dL_dmeans3D) {
+                gput_old(a.dL_dmeans3D, 3 * i, gm0, a3, o3[0]); gput_old(a.dL_dmeans3D, 3 * i + 1, gm1, a3, o3[1]);
+                gput_old(a.dL_dmeans3D, 3 * i + 2, gm2, a3, o3[2]);
+            }
             if (a.dL_dcov3D) {
 #pragma unroll
                 for (int k = 0; k < 6; ++k) gput(a.dL_dcov3D, 6 * i + k, gcov[k], acv);
@@ -1081,6 +1092,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         }
     }
     if constexpr (MC > 0) {  // the summed dL/dSH rows through LDS (over the coefficients), coalesced store
+        if (!a.dL_dsh) return;
         __syncthreads();
         if (live) {
 #pragma unroll

@@ -129,7 +129,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 12  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 13  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -320,13 +320,16 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
                                  activations=0, skip_unused=False, accumulate_into=None,
-                                 prepare_backward=False):
+                                 prepare_backward=False, needed=None):
     """Returns the 8 gradients of the upstream binding.  ``skip_unused``: gradients of inputs that
     were not given (colours under SH, cov3D under scales/rotations and vice versa) come back as
     empty tensors and their HBM writes are skipped.  ``accumulate_into``: optional sequence of 8
     tensors (or None) in output order; a given tensor (contiguous fp32 of the output's shape) receives
     ``tensor + gradient`` in place (the kernel's single add = autograd's accumulation) and is
-    returned in that slot."""
+    returned in that slot.  ``needed``: optional 8 booleans in output order; a False slot is not
+    computed into memory at all (NULL output, ABI 13) and comes back as None -- the autograd
+    Function passes ``needs_input_grad`` (train.py renders frozen Gaussians: only means3D,
+    rotations and means2D need a gradient there)."""
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
@@ -334,13 +337,14 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device
+    skip = tuple(k for k in range(8) if needed is not None and not needed[k])
     out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
-                                  accumulate_into)
+                                  accumulate_into, skip=skip)
     if P == 0:
         return out
     dpix = dL_dout_color.contiguous().float()
     keep.append(dpix)
-    grads = _Grads(*[t.data_ptr() if t.numel() else None for t in out], acc_bits)
+    grads = _Grads(*[t.data_ptr() if t is not None and t.numel() else None for t in out], acc_bits)
     alloc = _Allocator(dev)
     with _device_guard(dev):
         _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
@@ -377,10 +381,11 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
 
 def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations, scale_modifier,
                                        cov3D_precomp, sh, degree, activations=0, skip_unused=True,
-                                       accumulate_into=None, overwrite=()):
+                                       accumulate_into=None, overwrite=(), needed=None):
     """The per-Gaussian half over several views of the same Gaussians (gsr_backward_gaussians), on the
     current stream: returns the 8 gradients of ``rasterize_gaussians_backward`` summed over the views
-    (slot 0, dL/dmeans2D, is None: each view's goes to its own array).  ``views``: dicts with the
+    (slot 0, dL/dmeans2D, is None: each view's goes to its own array; ``needed`` as in
+    ``rasterize_gaussians_backward``).  ``views``: dicts with the
     view's ``viewmatrix``, ``projmatrix``, ``tanfovx``, ``tanfovy``, ``image_height``, ``image_width``,
     ``campos``, ``bg``, its ``radii``, ``geomBuffer``, ``scratch`` (from
     ``rasterize_gaussians_backward_render``) and ``num_rendered``, and optionally ``means2D_grad``, a
@@ -393,8 +398,9 @@ def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations
     dev = means3D.device
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=dev), scales, rotations,
                          scale_modifier, cov3D_precomp, keep, activations)
+    skip = (0,) + tuple(k for k in range(1, 8) if needed is not None and not needed[k])
     out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
-                                  accumulate_into, skip=(0,), overwrite=overwrite)
+                                  accumulate_into, skip=skip, overwrite=overwrite)
     if P == 0 or not views:
         return out
     cams = []

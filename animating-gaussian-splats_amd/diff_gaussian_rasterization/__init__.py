@@ -235,9 +235,13 @@ def _run_group(grp, created, post):
             views.append(dict(v, means2D_grad=m2, accumulate_means2D=not ow))
             if ow:
                 created.discard(id(v["means2D_grad"].leaf))
+        # slots without a target are gradients no input asked for (_try_defer queues a view only
+        # when every needed gradient has one): not computed into memory
+        needed = [k == 0 or grp["targets"][k] is not None for k in range(8)]
         _C.rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations,
                                               scale_modifier, cov3D, sh, degree, activations=act,
-                                              skip_unused=True, accumulate_into=targets, overwrite=over)
+                                              skip_unused=True, accumulate_into=targets, overwrite=over,
+                                              needed=needed)
         for k in over:  # written: later launches add into it
             created.discard(id(grp["targets"][k].leaf))
 
@@ -341,9 +345,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad,
                       lambda: _C.rasterize_gaussians_backward_render(*args, **kw)):
             return (None,) * 10  # every gradient is added into its leaf's .grad at the end of the pass
-        acc = [_accumulation_target(t, node) if ctx.needs_input_grad[i] else None
-               for t, i, node in zip(ctx.leaves, inputs, nodes)]
-        g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc, **kw))
+        need = [ctx.needs_input_grad[i] for i in inputs]
+        acc = [_accumulation_target(t, node) if n else None for t, n, node in zip(ctx.leaves, need, nodes)]
+        g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc, needed=need, **kw))
         for k, t in enumerate(acc):
             if t is not None:
                 g[k] = None  # already accumulated into the leaf's .grad
@@ -458,13 +462,15 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                for t, i, node in zip(ctx.leaves, inputs, nodes)]
         if acc[2] is not None and acc[2].shape != (means.shape[0], 1):
             acc[2] = None
+        needed = [i is not None and need[i] for i in inputs]
         (g_means2D, g_colors, g_opacity, g_means, _g_cov3D, g_sh, g_scales, g_rot) = \
             _C.rasterize_gaussians_backward(
                 rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
                 rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc, prepare_backward=ctx.prep)
-        done = [t is not None for t in acc]  # accumulated into the leaf's .grad: return None
+                activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc, prepare_backward=ctx.prep,
+                needed=needed)
+        done = [t is not None or not n for t, n in zip(acc, needed)]  # in the leaf's .grad / not needed: None
         return (None if done[3] else g_means, None if (done[0] or not need[1]) else g_means2D,
                 None if (done[5] or not sh.numel()) else g_sh,
                 None if (done[1] or not colors.numel()) else g_colors,

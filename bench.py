@@ -96,7 +96,8 @@ def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu, threads=0):
     from oracle import oracle as O
     import splat_scenes as S
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = O.set_threads(threads if threads > 0 else avail)
+    share = _cpu_quota() or avail
+    threads = O.set_threads(threads if threads > 0 else min(avail, share))
     a = {k: (v.detach().numpy() if isinstance(v, torch.Tensor) else v)
          for k, v in S.activated_inputs(params_cpu, cfg.sh_degree).items()}
     t0 = time.perf_counter()
@@ -107,11 +108,35 @@ def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu, threads=0):
     O.backward(st, dl_cpu.numpy())
     dt = time.perf_counter() - t0
     return {"value": round(cfg.P / dt / 1e6, 6), "unit": "Msplats/s", "cores": threads, "kind": "port",
-            "host_nproc": os.cpu_count(), "available_cpus": avail,
+            "host_nproc": os.cpu_count(), "available_cpus": avail, "cpu_quota": share,
             "sample": f"1 view of the same workload ({cfg.P} Gaussians, {cam_cpu.image_width}x"
                       f"{cam_cpu.image_height}, SH{cfg.sh_degree}) fwd+bwd by the C oracle "
-                      f"(oracle/gsr_oracle.c, OpenMP, {threads} threads; {avail} CPUs available to the "
-                      f"process, {os.cpu_count()} on the host), {dt:.2f} s"}
+                      f"(oracle/gsr_oracle.c, OpenMP, {threads} threads = the process's CPU share: "
+                      f"{avail} CPUs in its affinity mask, a cgroup quota of {share} CPUs, "
+                      f"{os.cpu_count()} on the host), {dt:.2f} s"}
+
+
+def _cpu_quota():
+    """CPUs this process's cgroup may use (cpu.max quota / period, rounded up), or None when
+    unlimited: the GPU box shows every host CPU in the affinity mask but grants a share of them, and
+    an OpenMP team of the whole host's size on that share runs slower than one of the share's size
+    (measured: 256 threads 2.80 s vs 16 threads 0.80 s for the same view)."""
+    import math
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, p = open(path).read().split()[:2]
+            if q != "max":
+                return max(1, math.ceil(int(q) / int(p)))
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, math.ceil(q / p))
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def _torch_calc_ssim(img1, img2):
@@ -505,27 +530,24 @@ def train_call_site(steps, cfg, cams, views, dl, dev, streams, sh):
         one(3 + it)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t) / steps * 1e3
-    # per-kernel device times of the same path (one stream, events on every phase; untimed)
+    # device time per launch of the path's kernels inside the same pipelined steps (HIP events on
+    # each kernel's launch stream, untimed steps)
     _C.profile_reset()
-    _C.profile_select(None)
+    _C.profile_select(["render_fwd", "render_bwd", "gauss_bwd"])
     _C.profile_enable(True)
-    for it in range(2):
-        p = dict(base)
-        p["means"] = base["means"] + delta[:, :3] * 0.01
-        p["rotation_quaternions"] = base["rotation_quaternions"] + delta[:, 3:] * 0.01
-        cur["p"] = p
-        rstep(views(it), solo=True)
-        delta.grad = None
+    for it in range(3):
+        one(3 + steps + it)
     torch.cuda.synchronize()
     _C.profile_enable(False)
-    phases = {ph: _C.profile_read(ph) for ph in PHASES}
+    _C.profile_select(None)
+    phases = {ph: _C.profile_read(ph) for ph in ("render_fwd", "render_bwd", "gauss_bwd")}
     rstep.close()
     nv = len(views(0))
     return {"features": "SH3 (shs)" if sh else "RGB (colors_precomp, as train.py renders)",
             "ms_per_step": round(ms, 4), "views_per_step": nv, "Msplats_per_s": round(nv * P / ms / 1e3, 2),
             "inputs": "non-leaf (frozen Gaussians, means/rotations = detach + 0.01 delta, per-view activations)",
             "backward": "immediate per-view (rasterizer inputs are not leaves)",
-            "solo_phase_ms_per_launch": {ph: round(v[0] / max(v[1], 1), 5) for ph, v in phases.items() if v[1]},
+            "in_step_kernel_ms_per_launch": {ph: round(v[0] / max(v[1], 1), 5) for ph, v in phases.items() if v[1]},
             "steps": steps}
 
 

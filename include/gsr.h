@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 12
+#define GSR_ABI_VERSION 13
 
 enum gsr_status {
     GSR_OK = 0,
@@ -115,10 +115,12 @@ enum gsr_grad_bits {
 };
 
 /* Gradient outputs of gsr_backward, in the order _C.rasterize_gaussians_backward returns them.
- * Every element of every non-NULL array is written (no pre-zeroing needed).  dL_dmeans2D,
- * dL_dopacity, dL_dmeans3D (and dL_dsh when shs are given) are required; dL_dcolors, dL_dcov3D,
- * dL_dscales and dL_drotations may be NULL when the caller does not need them (e.g. dL_dcolors
- * under SH colour, dL_dcov3D when scales/rotations are given): their HBM writes are skipped.
+ * Every element of every non-NULL array is written (no pre-zeroing needed).  Any of them may be
+ * NULL when the caller does not need it (ABI >= 13; before, dL_dmeans2D, dL_dopacity, dL_dmeans3D
+ * and dL_dsh were required): dL_dcolors under SH colour, dL_dcov3D when scales/rotations are given,
+ * and every input that does not require grad -- train.py renders frozen Gaussians
+ * (train.py:155-163 sets requires_grad = False) whose only live gradients are means3D, rotations
+ * and means2D.  The skipped arrays' HBM writes (and the SH coefficient rows) are not issued.
  * `accumulate` (gsr_grad_bits): the marked arrays already hold a gradient and receive
  * old + new (one fp32 add, what torch's AccumulateGrad computes) instead of new -- gradient
  * accumulation over the views of a step without a separate add pass. */

@@ -30,8 +30,8 @@ pytestmark = pytest.mark.gpu
 
 # measured outside-tolerance fractions x 4 (profiles/r03_parity_flips.json)
 ALLOW = {
-    "C3_summed": dict(pix=1e-5, grad=1e-4),
-    "C5_view": dict(pix=1e-5, grad=1e-4),
+    "C3_summed": dict(pix=5.8e-6, grad=8.4e-5),   # measured 1.45e-6 / 2.1e-5
+    "C5_view": dict(pix=5.2e-6, grad=2.4e-5),     # measured 1.29e-6 / 6.0e-6
 }
 VIEWS = [0, 1, 2, 3, 4]  # the bench's first step: rig cameras 0-4 (height -0.8, yaw 0..160)
 
