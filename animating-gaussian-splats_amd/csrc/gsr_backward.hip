@@ -120,6 +120,18 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
 #define GSR_BWD_WAVES 4  // items (one wave each) per workgroup
 #endif
 constexpr int kBwdWaves = GSR_BWD_WAVES;
+#ifndef GSR_BWD_TRED
+#define GSR_BWD_TRED 0  // transposed pair reduction: pairs per LDS group (0: per-pair DPP reduction; 4-16 measured slower)
+#endif
+// Transposed reduction (GSR_BWD_TRED = G): a walked pair's 6 per-lane sums are folded over the wave's
+// lane halves and rows (3 permlane32 + 2 permlane16 swaps: 16 column sums of each value) and parked in
+// LDS; every G pairs the wave reads them back transposed -- 64 / G lanes per pair, each summing
+// 16 G / 64 columns with the column weights dx, dx^2, then a log2(64 / G)-stage DPP sum -- and
+// writes each pair's 9 sums into its s_out slot.  Replaces the per-pair weighting + 3 x 3 DPP row
+// stages + LDS atomics of wave_pair_sums with work spread over all lanes (fixed order: bitwise
+// reproducible).
+constexpr int kTred = GSR_BWD_TRED;
+constexpr int kTredF = 96;  // floats per parked pair: 4 column-sum rows (64) + cs1 / cs2 columns (32)
 __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
@@ -136,11 +148,19 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     // workgroups).
     __shared__ float4 s_a_all[64 * kBwdWaves], s_b_all[64 * kBwdWaves], s_c_all[64 * kBwdWaves];
     __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
+#if GSR_BWD_TRED
+    __shared__ float s_park_all[kTred * kTredF * kBwdWaves];  // parked column sums (transposed reduction)
+    __shared__ uint32_t s_slot_all[kTred * kBwdWaves];        // staged index j of each parked pair
+#endif
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t item = blockIdx.x * kBwdWaves + wv;
     if (item >= items[0].x) return;  // the launch covers the item bound
     float4 *s_a = s_a_all + 64 * wv, *s_b = s_b_all + 64 * wv, *s_c = s_c_all + 64 * wv;
     float *s_out = s_out_all + 64 * kPartial * wv;
+#if GSR_BWD_TRED
+    float *s_park = s_park_all + kTred * kTredF * wv;
+    uint32_t *s_slot = s_slot_all + kTred * wv;
+#endif
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     uint32_t tr_evals = 0, tr_reds = 0;  // (pair, quarter) evaluations and wave reductions
@@ -213,8 +233,64 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     const int row = lane >> 4;
     // s_out slots per pair: 0 sum dx S0, 1 sum S1, 2 sum dx^2 S0, 3 sum dx S1, 4 sum S4, 5 sum S0,
     // 6..8 sum cs (the first five still to be scaled by the opacity); wave_pair_sums row map:
+#if !GSR_BWD_TRED
     const int xslot = (row == 0) ? 0 : (row == 1) ? 4 : (row == 2) ? 1 : 6;
     const int yslot = (row == 0) ? 2 : (row == 1) ? 7 : (row == 2) ? 3 : 8;
+#else
+    // transposed reduction: lane l reads parked pair l / kLps, columns (l % kLps) * kCpl ...
+    constexpr int kLps = 64 / kTred, kCpl = 16 / kLps;
+    static_assert(kTred >= 4 && kTred <= 16 && (kTred & (kTred - 1)) == 0, "GSR_BWD_TRED: 4, 8 or 16");
+    const int t_slot = lane / kLps, t_c0 = (lane % kLps) * kCpl;
+    int parked = 0;  // wave-uniform: pairs parked since the last flush
+    auto flush = [&](int n) {
+        wave_lds_sync();
+        if (t_slot < n) {
+            const uint32_t j = s_slot[t_slot];
+            const float gx = s_a[j].x;
+            const float *pk = s_park + t_slot * kTredF;
+            float *o = s_out + j * kPartial;
+            // three passes of three sums each (few live registers: the walk's per-pixel state is live)
+            auto reduce3 = [&](float a, float b, float c, int s0, int s1, int s2) {
+#pragma unroll
+                for (int d = 1; d < kLps; d <<= 1) {  // the slot's lanes are consecutive: xor butterfly
+                    a += __shfl_xor(a, d, 64);
+                    b += __shfl_xor(b, d, 64);
+                    c += __shfl_xor(c, d, 64);
+                }
+                if ((lane % kLps) == 0) { o[s0] = a; o[s1] = b; o[s2] = c; }
+            };
+            {   // row 0 (S0): sum, sum dx, sum dx^2
+                float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+                for (int k = 0; k < kCpl; ++k) {
+                    const float dx = gx - (tx0 + (float)(t_c0 + k));  // = pair_x's dx of the column
+                    const float v = pk[t_c0 + k], u = dx * v;
+                    a += v; b += u; c = fmaf(dx, u, c);
+                }
+                reduce3(a, b, c, 5, 0, 2);
+            }
+            {   // rows 1 (S4) and 2 (S1): sum S4, sum S1, sum dx S1
+                float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+                for (int k = 0; k < kCpl; ++k) {
+                    const float dx = gx - (tx0 + (float)(t_c0 + k));
+                    const float v = pk[32 + t_c0 + k];
+                    a += pk[16 + t_c0 + k]; b += v; c = fmaf(dx, v, c);
+                }
+                reduce3(a, b, c, 4, 1, 3);
+            }
+            {   // colour: row 3 (cs0) and the parked cs1 / cs2 columns
+                float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+                for (int k = 0; k < kCpl; ++k) {
+                    a += pk[48 + t_c0 + k]; b += pk[64 + t_c0 + k]; c += pk[80 + t_c0 + k];
+                }
+                reduce3(a, b, c, 6, 7, 8);
+            }
+        }
+        wave_lds_sync();
+    };
+#endif
     // the batch ending at `e` (slots [max(e - 64, s0), e)): lane j's slot, its Gaussian's whole render
     // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
     // behind the current batch's pairs
@@ -338,6 +414,22 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             tr_evals += __builtin_popcount(qm);
             tr_reds += __ballot(any) ? 1u : 0u;
 #endif
+#if GSR_BWD_TRED
+            if (!GSR_BWD_ANY || __ballot(any)) {
+                // fold the 6 sums to 16 column sums each and park them; reduced every kTred pairs
+                const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(cs1, cs2);
+                const float rA = fold16(pA, pB);  // rows [S0, S4, S1, cs0]
+                const float rC = fold16(pC, pC);  // rows [cs1, cs1, cs2, cs2]
+                float *pk = s_park + parked * kTredF;
+                pk[lane] = rA;
+                if (!(row & 1)) pk[64 + (row >> 1) * 16 + (lane & 15)] = rC;
+                if (lane == 0) s_slot[parked] = (uint32_t)j;
+                if (++parked == kTred) {
+                    flush(kTred);
+                    parked = 0;
+                }
+            }
+#else
             if (!GSR_BWD_ANY || __ballot(any)) {
                 // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
                 const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
@@ -349,7 +441,14 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
                     if (lane < kRedLanes) lds_add(o + 5, sm.Z);
                 }
             }
+#endif
         }
+#if GSR_BWD_TRED
+        if (parked) {
+            flush(parked);
+            parked = 0;
+        }
+#endif
         wave_lds_sync();
         if (lane < cnt) {
             const float *s2 = s_out + lane * kPartial;

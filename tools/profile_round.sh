@@ -4,11 +4,11 @@
 # passes of SQ counters (VALU / LDS / SALU activity) for the compute-bound kernels.  Same bench
 # arguments in every pass, so the per-launch averages describe the command bench.py reports on.
 # usage (on the box, from the repo root): bash tools/profile_round.sh <tag> [bench args...]
-# TIMED_RANGE (default 40:140 = bench defaults: (warmup 5 + probe 3) x 5 views .. + 20 steps x 5 views)
+# TIMED_RANGE (default 40:140 = (warmup 5 + probe 3) x 5 views .. + 20 steps x 5 views; BENCH_LEGS pins those counts)
 # outputs: gpurun_out/prof_<tag>/{trace,fetch,write,sq1,sq2}/ raw CSV, trace_summary.txt, hbm_pmc.json, sq_pmc.json
 set -u
 tag=${1:-r01}; shift || true
-BENCH_LEGS="--call-site-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0"
+BENCH_LEGS="--call-site-steps 0 --train-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0 --steps 20 --warmup 5"
 R=$(pwd)
 O=$R/gpurun_out/prof_$tag
 mkdir -p "$O"
