@@ -266,13 +266,51 @@ int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     return n;
 }
 
-int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
-                float *out_color, float *out_depth, int *out_radii, int *out_num_rendered,
-                void *stream) {
+}  // extern "C"
+
+namespace {
+// Pair-count history for the speculative enqueue, per (device, P, W, H): the largest K seen and
+// whether a list needed the merge sort.  A forward with history queues its post-scan kernels against
+// a BINNING capacity of 1.25 x that K (+ 64 K pairs) before reading K back, so the GPU never waits for
+// the host between k_bin_scan and k_bin_emit; the kernels check k_bin_scan's verdict on the device
+// and the host redoes the post-scan part with the exact K when it failed (a larger K, a long list).
+struct SpecKey {
+    int dev, P, W, H;
+    bool operator==(const SpecKey &o) const { return dev == o.dev && P == o.P && W == o.W && H == o.H; }
+};
+struct SpecKeyHash {
+    size_t operator()(const SpecKey &k) const {
+        return ((size_t)k.dev * 1000003u) ^ ((size_t)k.P * 2654435761u) ^ ((size_t)k.W << 20) ^ (size_t)k.H;
+    }
+};
+struct SpecStat { uint32_t max_k = 0; bool long_lists = false; };
+std::mutex g_spec_mu;
+std::unordered_map<SpecKey, SpecStat, SpecKeyHash> g_spec;
+int g_spec_hits = 0, g_spec_misses = 0;
+
+uint32_t spec_capacity(const SpecKey &key) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    auto it = g_spec.find(key);
+    if (it == g_spec.end() || it->second.long_lists) return 0;
+    const uint64_t c = (uint64_t)it->second.max_k + it->second.max_k / 4 + 65536;
+    return (uint32_t)std::min<uint64_t>((c + 4095) & ~uint64_t(4095), 0x7FFFFFFFu);
+}
+void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    SpecStat &st = g_spec[key];
+    st.max_k = std::max(st.max_k, K);
+    st.long_lists = long_lists;
+    if (outcome > 0) ++g_spec_hits;
+    if (outcome < 0) ++g_spec_misses;
+}
+
+int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                 float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, bool speculate,
+                 void *stream) {
     HostPhase host_total("host_forward");
     int rc = check_common(cam, g, true);
     if (rc) return rc;
-    if (!alloc || !out_color || !out_depth || !out_num_rendered || (g->P > 0 && !out_radii))
+    if (!alloc || !out_color || !out_depth || !info || (g->P > 0 && !out_radii))
         return fail(GSR_ERR_ARG, "gsr_forward: missing output or allocator");
     hipStream_t s = (hipStream_t)stream;
     FwdArgs a;
@@ -285,7 +323,9 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     if (!geom || !img) return fail(GSR_ERR_ALLOC, "allocation callback failed (geom/image)");
     carve_geom(a, geom);
     carve_image(a, img);
-    *out_num_rendered = 0;
+    info->num_rendered = 0;
+    info->binning_layout = 0;
+    info->speculated = 0;
     if (a.P == 0) {  // reference: colour/depth stay zero (no background) when there are no Gaussians
         HIP_TRY(launch_zero(out_color, 3 * npix, s));
         HIP_TRY(launch_zero(out_depth, npix, s));
@@ -293,12 +333,33 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
         if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning)");
         return GSR_OK;
     }
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const SpecKey key{dev, a.P, a.W, a.H};
+    const uint32_t cap = speculate ? spec_capacity(key) : 0u;
+    a.spec_cap = cap;
+    const int T = a.gx * a.gy;
     { Phase ph(s, "preprocess"); HIP_TRY(launch_preprocess(a, s)); }
     { Phase ph(s, "bin_count"); HIP_TRY(launch_bin_count(a, s)); }
     HostWord hw = pinned_word();
     if (!hw.h) return fail(GSR_ERR_HIP, "hipHostMalloc(mapped) failed");
     __atomic_store_n(hw.h, kNoValue, __ATOMIC_SEQ_CST);
     { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, hw.d, s)); }
+    const size_t spec_item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;
+    if (cap) {  // speculative: the post-scan kernels are queued now, against the capacity
+        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)cap).total + spec_item_bytes);
+        if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, capacity %u)", cap);
+        carve_binning(a, bin, (int)cap);
+        a.spec_ok = a.meta + 1;
+        { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, 0, s)); }
+        { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, 0, 0, 0, nullptr, s)); }
+        { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
+        if (GSR_FWD_ITEMS && g->prepare_backward) {
+            Phase ph(s, "bwd_items");
+            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.ranges, a.tile_maxc,
+                                         (uint2 *)(bin + BinningLayout((int)cap).total), s, a.spec_ok));
+        }
+    }
     uint32_t K;
     {
         HostPhase hp("host_wait_K");
@@ -320,15 +381,23 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
         }
     }
     if (K > 0x7FFFFFFFu) return fail(GSR_ERR_UNSUPPORTED, "num_rendered overflow");
-    *out_num_rendered = (int)K;
+    info->num_rendered = (int)K;
     // tiles to sort outside the render: [1] up to kSortCap pairs, [2] longer (merge sort), [3] the
     // longest list (merge passes); the latter need a temporary copy of the pair records
     const uint32_t n_mid = __atomic_load_n(hw.h + 1, __ATOMIC_ACQUIRE);
     const uint32_t n_vlong = __atomic_load_n(hw.h + 2, __ATOMIC_ACQUIRE);
     const uint32_t max_n = __atomic_load_n(hw.h + 3, __ATOMIC_ACQUIRE);
+    if (cap && K <= cap && n_vlong == 0) {  // the device took the same verdict: the queued work stands
+        info->binning_layout = (int)cap;
+        info->speculated = 1;
+        spec_record(key, K, false, +1);
+        return GSR_OK;
+    }
+    // exact path (also the redo of a failed speculation: its queued kernels returned at once)
+    a.spec_ok = nullptr;
     // BINNING = the binning arrays, [the backward's item list], [the long-list merge buffer]
     const size_t bin_bytes = BinningLayout((int)K).total;
-    const size_t item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)K, a.gx * a.gy) : 0;
+    const size_t item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)K, T) : 0;
     const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
     char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, bin_bytes + item_bytes + tmp_bytes);
     if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
@@ -338,12 +407,44 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // the backward's item list, built here, off its critical path
         Phase ph(s, "bwd_items");
-        HIP_TRY(launch_bwd_items_raw((int)K, a.gx * a.gy, a.ranges, a.tile_maxc, (uint2 *)(bin + bin_bytes), s));
+        HIP_TRY(launch_bwd_items_raw((int)K, T, a.ranges, a.tile_maxc, (uint2 *)(bin + bin_bytes), s));
     }
+    info->binning_layout = (int)K;
+    spec_record(key, K, n_vlong > 0, cap ? -1 : 0);
+    return GSR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                float *out_color, float *out_depth, int *out_radii, int *out_num_rendered,
+                void *stream) {
+    if (!out_num_rendered) return fail(GSR_ERR_ARG, "gsr_forward: missing output or allocator");
+    *out_num_rendered = 0;
+    gsr_forward_info info;
+    const int rc = forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, &info, false, stream);
+    *out_num_rendered = info.num_rendered;
+    return rc;
+}
+
+int gsr_forward_info_call(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                          float *out_color, float *out_depth, int *out_radii, int speculate, gsr_forward_info *info,
+                          void *stream) {
+    if (!info) return fail(GSR_ERR_ARG, "gsr_forward_info_call: null info");
+    return forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, info, speculate != 0, stream);
+}
+
+int gsr_spec_stats(int *hits, int *misses, int reset) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    if (hits) *hits = g_spec_hits;
+    if (misses) *misses = g_spec_misses;
+    if (reset) { g_spec.clear(); g_spec_hits = g_spec_misses = 0; }
     return GSR_OK;
 }
 
 }  // extern "C"
+
 
 namespace {
 // The per-pixel half of the backward (bwd items + k_render_bwd): BwdArgs of the view and its SCRATCH
@@ -358,7 +459,10 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     fill_common(f, cam, g);
     carve_geom(f, (char *)geom);
     carve_image(f, (char *)image);
-    carve_binning(f, (char *)binning, num_rendered);
+    // the BINNING layout the forward used: its capacity when it enqueued speculatively (gsr_forward_info)
+    const int layout = g->binning_layout > 0 ? g->binning_layout : num_rendered;
+    if (layout < num_rendered) return fail(GSR_ERR_ARG, "binning_layout %d < num_rendered %d", layout, num_rendered);
+    carve_binning(f, (char *)binning, layout);
     memset(&a, 0, sizeof(a));
     a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
     a.act = f.act;
@@ -379,7 +483,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.part = (float4 *)(scr + SL.part);
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // built by the forward, after the binning arrays
-        a.items = (uint2 *)((char *)binning + BinningLayout(num_rendered).total);
+        a.items = (uint2 *)((char *)binning + BinningLayout(layout).total);
     } else {
         a.items = (uint2 *)(scr + SL.items);
         Phase ph(s, "bwd_items");

@@ -29,9 +29,10 @@ __device__ uint64_t *g_trace_bwd;
 constexpr uint32_t kItemStartCost = 64;  // init loads + first gathers, in (pair, quarter) steps
 __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restrict__ ranges,
                                                     const uint32_t *__restrict__ tile_maxc,
-                                                    uint2 *__restrict__ items) {
+                                                    uint2 *__restrict__ items, const uint32_t *__restrict__ spec_ok) {
     __shared__ uint32_t s_hist[kOrderBuckets];
     __shared__ uint32_t s_red[16];
+    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
     for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
     constexpr uint32_t kMaxCost = 4u * kSeg + kItemStartCost;
     constexpr uint32_t kShift = kMaxCost >= (uint32_t)kOrderBuckets ? 32 - __builtin_clz(kMaxCost / kOrderBuckets) : 0;
@@ -130,8 +131,10 @@ constexpr int kBwdWaves = GSR_BWD_WAVES;
 // writes each pair's 9 sums into its s_out slot.  Replaces the per-pair weighting + 3 x 3 DPP row
 // stages + LDS atomics of wave_pair_sums with work spread over all lanes (fixed order: bitwise
 // reproducible).
+#if GSR_BWD_TRED
 constexpr int kTred = GSR_BWD_TRED;
 constexpr int kTredF = 96;  // floats per parked pair: 4 column-sum rows (64) + cs1 / cs2 columns (32)
+#endif
 __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
@@ -1206,9 +1209,9 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 
 // ==========================================================================================
 hipError_t launch_bwd_items_raw(int K, int T, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
-                                hipStream_t s) {
+                                hipStream_t s, const uint32_t *spec_ok) {
     if (K == 0) return hipSuccess;
-    k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items);
+    k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items, spec_ok);
     return hipGetLastError();
 }
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {

@@ -21,6 +21,8 @@
 #include "gsr_common.h"
 #include "gsr_internal.h"
 
+#include <algorithm>
+
 namespace gsr {
 
 #ifdef GSR_TRACE
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
                                                    uint32_t *host_words,
                                                    uint32_t *__restrict__ tile_order,
                                                    uint32_t *__restrict__ sort_lists,
-                                                   uint32_t *__restrict__ seg_off) {
+                                                   uint32_t *__restrict__ seg_off, uint32_t cap) {
     __shared__ uint32_t s_red[16];
     __shared__ uint32_t s_hist[kOrderBuckets];
     __shared__ uint32_t s_cls[3];
@@ -279,6 +281,10 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
         if ((int)threadIdx.x < NB) block_off[threadIdx.x] = bex;
         if (threadIdx.x == 0) {
             meta[0] = K;
+            // speculative enqueue (gsr_forward_info): the kernels queued before the host read K run
+            // only when the BINNING capacity holds K and no list needs the merge sort
+            meta[1] = (cap && K <= cap && s_cls[1] == 0u) ? 1u : 0u;
+            meta[2] = s_cls[0];
             if (host_words) {
                 for (int q = 0; q < 3; ++q)
                     __hip_atomic_store(host_words + 1 + q, s_cls[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -334,6 +340,8 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
     __syncthreads();
     if (threadIdx.x == 0) {
         meta[0] = carry;
+        meta[1] = (cap && carry <= cap && s_cls[1] == 0u) ? 1u : 0u;
+        meta[2] = s_cls[0];
         // publish straight into host-mapped pinned memory (the host spins on word 0): no copy
         // kernel, no stream synchronisation.  K goes last with system-scope release.
         if (host_words) {
@@ -359,9 +367,11 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
                                                   uint32_t *__restrict__ tile_cursor,
                                                   uint32_t *__restrict__ goff,
                                                   uint4 *__restrict__ pairs, uint32_t K,
-                                                  const uint32_t *__restrict__ chunk_off) {
+                                                  const uint32_t *__restrict__ chunk_off,
+                                                  const uint32_t *__restrict__ spec_ok) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
     __shared__ uint32_t s_red[16];
+    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: the host redoes it
     const int b = blockIdx.x;
     const int g0 = b * CH, g1 = min(P, g0 + CH);
     GSR_EMIT_STAMP(0);
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
             }
         }
     }
-    if (b == gridDim.x - 1 && threadIdx.x == 0) goff[P] = K;
+    if (b == gridDim.x - 1 && threadIdx.x == 0) goff[P] = spec_ok ? spec_ok[-1] : K;  // meta[0] = K
 #ifdef GSR_TRACE
     __syncthreads();
     GSR_EMIT_STAMP(3);
@@ -529,22 +539,33 @@ __device__ inline void block_sort_tile(int n, uint32_t start, const uint4 *__res
 
 // Tiles longer than kFwdSortCap and at most kSortCap pairs (one 512-thread block each, launched only
 // for those tiles): the register + LDS hybrid of block_sort_tile over 8 waves (4 or 8 keys per lane).
+// Launched with one block per such tile (nlist = n_mid known on the host), or -- speculative
+// enqueue, before the host knows the count -- with a fixed grid whose blocks loop over the list
+// count k_bin_scan left in meta[2] (spec_ok = meta + 1).
 __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__restrict__ tiles,
                                                     const uint2 *__restrict__ ranges,
                                                     uint4 *__restrict__ pairs,
                                                     uint32_t *__restrict__ point_list,
-                                                    uint32_t *__restrict__ slot_emit) {
+                                                    uint32_t *__restrict__ slot_emit, uint32_t nlist,
+                                                    const uint32_t *__restrict__ spec_ok) {
     __shared__ uint64_t s_keys[kSortCap];
     __shared__ uint32_t s_vals[kSortCap];
-    const int tile = (int)tiles[blockIdx.x];
-    const uint2 rg = ranges[tile];
-    const int n = (int)(rg.y - rg.x);
+    if (spec_ok) {
+        if (*spec_ok == 0u) return;
+        nlist = spec_ok[1];  // meta[2]: tiles of kFwdSortCap < n <= kSortCap pairs
+    }
     static_assert(kSortCap == 8 * 64 * 8, "k_tile_sort: 8 waves x 64 lanes x 8 keys");
-    if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, pairs, s_keys, s_vals);
-    else block_sort_tile<8, 8>(n, rg.x, pairs, s_keys, s_vals);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        point_list[rg.x + i] = (uint32_t)s_keys[i];
-        slot_emit[rg.x + i] = s_vals[i];
+    for (uint32_t li = blockIdx.x; li < nlist; li += gridDim.x) {
+        const int tile = (int)tiles[li];
+        const uint2 rg = ranges[tile];
+        const int n = (int)(rg.y - rg.x);
+        if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, pairs, s_keys, s_vals);
+        else block_sort_tile<8, 8>(n, rg.x, pairs, s_keys, s_vals);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            point_list[rg.x + i] = (uint32_t)s_keys[i];
+            slot_emit[rg.x + i] = s_vals[i];
+        }
+        __syncthreads();  // the LDS keys are reused by the block's next list
     }
 }
 
@@ -664,7 +685,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
     float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
-    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state) {
+    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok) {
     __shared__ uint64_t s_key[kFwdSortCap];
     __shared__ union {
         uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
@@ -677,6 +698,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
+    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
     const int tile = (int)tile_order[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -903,7 +925,7 @@ hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s
     const BinGrid bg(a.P);
     k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
                                   a.block_sums, a.block_off, a.meta, host_words, a.tile_order_f,
-                                  a.sort_lists, a.seg_off);
+                                  a.sort_lists, a.seg_off, a.spec_cap);
     return hipGetLastError();
 }
 
@@ -912,9 +934,9 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off);
+        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off, a.spec_ok);
     else
-        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off);
+        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off, a.spec_ok);
     return hipGetLastError();
 }
 
@@ -923,7 +945,13 @@ hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, 
     // lists of up to kFwdSortCap pairs are sorted inside k_render_fwd; up to kSortCap by one block
     // per tile; longer ones by chunk sorts + merge passes
     const int T = a.gx * a.gy;
-    if (n_mid) k_tile_sort<<<n_mid, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs, a.point_list, a.slot_emit);
+    if (a.spec_ok) {  // speculative: the count is on the device; blocks loop over it (none here: n_vlong == 0)
+        k_tile_sort<<<std::min(T, kSpecSortBlocks), 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs, a.point_list,
+                                                                 a.slot_emit, 0u, a.spec_ok);
+        return hipGetLastError();
+    }
+    if (n_mid) k_tile_sort<<<n_mid, 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs, a.point_list, a.slot_emit,
+                                                 n_mid, nullptr);
     if (n_vlong) {
         const dim3 grid((unsigned)div_up((int)max_n, kSortCap), n_vlong);
         k_chunk_sort<<<grid, 512, 0, s>>>(T, a.sort_lists, a.ranges, a.pairs);
@@ -945,7 +973,7 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                                    a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
-                                   a.tile_maxc, a.seg_off, a.seg_state);
+                                   a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok);
     return hipGetLastError();
 }
 

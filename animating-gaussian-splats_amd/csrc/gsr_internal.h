@@ -22,7 +22,13 @@ struct FwdArgs {
     uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
     int *radii; float *out_color; float *out_depth;
+    // speculative enqueue (gsr_forward_info with speculate): the BINNING capacity the post-scan kernels
+    // were queued with before the host read K (0: exact path), and the device flag they check
+    // (meta + 1, written by k_bin_scan; nullptr: exact path)
+    uint32_t spec_cap; const uint32_t *spec_ok;
 };
+// blocks of the speculative k_tile_sort launch (they loop over the device-side list count)
+constexpr int kSpecSortBlocks = 512;
 
 struct BwdArgs {
     int P, D, M, W, H, gx, gy, K, act;
@@ -60,7 +66,7 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s);
 hipError_t launch_bwd_items_raw(int K, int T, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
-                                hipStream_t s);
+                                hipStream_t s, const uint32_t *spec_ok = nullptr);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 

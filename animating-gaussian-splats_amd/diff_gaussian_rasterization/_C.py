@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
+    "gsr_forward_info_call", "gsr_spec_stats",
 )
 
 
@@ -51,7 +52,12 @@ class _Gaussians(ctypes.Structure):
                 ("shs", ctypes.c_void_p), ("colors_precomp", ctypes.c_void_p),
                 ("opacities", ctypes.c_void_p), ("scales", ctypes.c_void_p),
                 ("rotations", ctypes.c_void_p), ("cov3D_precomp", ctypes.c_void_p),
-                ("activations", ctypes.c_int), ("prepare_backward", ctypes.c_int)]
+                ("activations", ctypes.c_int), ("prepare_backward", ctypes.c_int),
+                ("binning_layout", ctypes.c_int)]
+
+
+class _ForwardInfo(ctypes.Structure):  # gsr_forward_info (ABI 14)
+    _fields_ = [("num_rendered", ctypes.c_int), ("binning_layout", ctypes.c_int), ("speculated", ctypes.c_int)]
 
 
 class _Grads(ctypes.Structure):
@@ -84,6 +90,11 @@ def load_library():
     L.gsr_forward.restype = i
     L.gsr_forward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), _ALLOC_FN, vp,
                               vp, vp, vp, ctypes.POINTER(i), vp]
+    L.gsr_forward_info_call.restype = i
+    L.gsr_forward_info_call.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), _ALLOC_FN, vp,
+                                        vp, vp, vp, i, ctypes.POINTER(_ForwardInfo), vp]
+    L.gsr_spec_stats.restype = i
+    L.gsr_spec_stats.argtypes = [ctypes.POINTER(i), ctypes.POINTER(i), i]
     L.gsr_backward.restype = i
     L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
                                vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]
@@ -129,7 +140,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 13  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 14  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -234,7 +245,7 @@ def _mat16(m):
 
 
 def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier, cov3D, keep,
-               activations=0, prepare_backward=False):
+               activations=0, prepare_backward=False, binning_layout=0):
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     P = means3D.size(0)
@@ -244,17 +255,20 @@ def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_mo
     M = sh.size(1) if sh is not None and sh.numel() else 0
     return _Gaussians(P, int(degree), M, float(scale_modifier), _ptr(means3D), _ptr(sh), _ptr(colors),
                       _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(cov3D),
-                      int(activations), int(bool(prepare_backward))), P, M
+                      int(activations), int(bool(prepare_backward)), int(binning_layout or 0)), P, M
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
                         image_width, sh, degree, campos, prefiltered, debug=False, activations=0,
-                        prepare_backward=False):
+                        prepare_backward=False, speculate=False, info=None):
     """``activations`` (ACT_* bits): opacity / scales / rotations hold the raw parameters of
     shared.py:29-42 and are activated inside the kernels (0 = the reference's interface).
     ``prepare_backward``: a backward will follow; the forward also builds its work-item list (the
-    backward calls must then pass the same flag)."""
+    backward calls must then pass the same flag).  ``speculate``: queue the post-scan kernels before
+    num_rendered is read back (gsr_forward_info_call, include/gsr.h); ``info`` (a dict) receives
+    ``num_rendered``, ``binning_layout`` (pass it to the backward calls and decode_buffers) and
+    ``speculated``."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
@@ -267,13 +281,23 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
     radii = torch.empty((P,), dtype=torch.int32, device=dev)  # preprocess writes every entry
     alloc = _Allocator(dev)
-    nr = ctypes.c_int(0)
+    fi = _ForwardInfo(0, 0, 0)
     with _device_guard(dev):  # launches go to dev even when another device is current
-        _check(L.gsr_forward(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
-                             depth.data_ptr(), radii.data_ptr() if P else None, ctypes.byref(nr),
-                             _stream_ptr(dev)))
+        _check(L.gsr_forward_info_call(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
+                                       depth.data_ptr(), radii.data_ptr() if P else None, int(bool(speculate)),
+                                       ctypes.byref(fi), _stream_ptr(dev)))
+    if info is not None:
+        info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated))
     b = alloc.buffers
-    return nr.value, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
+    return fi.num_rendered, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
+
+
+def speculation_stats(reset=False):
+    """(stood, redone) counts of speculative forwards since the last reset; ``reset`` also clears the
+    pair-count history the capacities come from."""
+    h, m = ctypes.c_int(0), ctypes.c_int(0)
+    _check(load_library().gsr_spec_stats(ctypes.byref(h), ctypes.byref(m), int(bool(reset))))
+    return h.value, m.value
 
 
 def _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused, accumulate_into,
@@ -320,7 +344,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
                                  activations=0, skip_unused=False, accumulate_into=None,
-                                 prepare_backward=False, needed=None):
+                                 prepare_backward=False, needed=None, binning_layout=0):
     """Returns the 8 gradients of the upstream binding.  ``skip_unused``: gradients of inputs that
     were not given (colours under SH, cov3D under scales/rotations and vice versa) come back as
     empty tensors and their HBM writes are skipped.  ``accumulate_into``: optional sequence of 8
@@ -333,7 +357,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
-                         rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward)
+                         rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward,
+                         binning_layout)
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device
@@ -356,14 +381,16 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
 def rasterize_gaussians_backward_render(background, means3D, radii, colors, scales, rotations,
                                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                         tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
-                                        binningBuffer, imageBuffer, activations=0, prepare_backward=False):
+                                        binningBuffer, imageBuffer, activations=0, prepare_backward=False,
+                                        binning_layout=0):
     """The per-pixel half of ``rasterize_gaussians_backward`` (gsr_backward_render): returns the
     view's SCRATCH byte buffer holding its per-(tile, Gaussian) gradient records, for
     ``rasterize_gaussians_backward_views``."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
-                         rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward)
+                         rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward,
+                         binning_layout)
     H, W = dL_dout_color.shape[-2], dL_dout_color.shape[-1]
     cam = _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, H, W, campos, background, False, keep)
     dev = means3D.device
@@ -475,11 +502,12 @@ def profile_read(phase=None):
     return tot.value, cnt.value
 
 
-def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
-    """Typed views of the arrays inside the forward buffers (for parity tests / debugging)."""
+def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer, binning_layout=0):
+    """Typed views of the arrays inside the forward buffers (for parity tests / debugging);
+    ``binning_layout``: the forward's info["binning_layout"] when it enqueued speculatively."""
     L = load_library()
     offs = (ctypes.c_size_t * 14)()
-    L.gsr_buffer_offsets(int(P), int(W), int(H), int(num_rendered), offs, 14)
+    L.gsr_buffer_offsets(int(P), int(W), int(H), int(binning_layout or num_rendered), offs, 14)
     o = list(offs)
     T = ((W + 15) // 16) * ((H + 15) // 16)
     K = int(num_rendered)

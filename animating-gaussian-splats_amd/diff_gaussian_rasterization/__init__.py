@@ -24,7 +24,8 @@ from torch.autograd.graph import get_gradient_edge
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_parameters", "set_deferred_backward", "pending_views", "clear_pending"]
+           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "pending_views",
+           "clear_pending"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -148,7 +149,10 @@ def _fresh_target(t, created, post):
 # (node.register_hook / register_prehook, e.g. DDP's reducer) cannot be seen from Python: such
 # callers read .grad during the pass and must run with set_deferred_backward(False).
 _defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0",
-          "fresh": os.environ.get("GSR_FRESH_GRADS", "1") != "0"}
+          "fresh": os.environ.get("GSR_FRESH_GRADS", "1") != "0",
+          # forwards queue their post-scan kernels before num_rendered is read back (include/gsr.h,
+          # gsr_forward_info_call): the stream does not idle while the host reads K and launches
+          "speculate": os.environ.get("GSR_SPECULATE", "1") != "0"}
 _pending_lock = threading.Lock()
 _pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
 _queued = set()  # graph tasks whose flush callback is queued
@@ -158,6 +162,14 @@ def set_deferred_backward(on: bool) -> bool:
     """Enable / disable the deferred multi-view per-Gaussian backward; returns the previous setting."""
     prev = _defer["on"]
     _defer["on"] = bool(on)
+    return prev
+
+
+def set_speculative_forward(on: bool) -> bool:
+    """Enable / disable the forward's speculative enqueue (gsr_forward_info_call); returns the
+    previous setting.  The outputs are bitwise the same either way."""
+    prev = _defer["speculate"]
+    _defer["speculate"] = bool(on)
     return prev
 
 
@@ -313,10 +325,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         # a backward can follow (grad mode at the call, an input requiring grad): the forward
         # prepares it
         ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)
+        info = {}
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = \
-            _C.rasterize_gaussians(*args, prepare_backward=ctx.prep)
+            _C.rasterize_gaussians(*args, prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info)
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
+        ctx.binning_layout = info["binning_layout"]
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
         ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
         ctx.tensor_pos = _tensor_positions((means3D, means2D, sh, colors_precomp, opacities, scales,
@@ -337,7 +351,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
                 cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                 sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
-        kw = {"prepare_backward": ctx.prep}
+        kw = {"prepare_backward": ctx.prep, "binning_layout": ctx.binning_layout}
         inputs = (1, 3, 4, 0, 7, 2, 5, 6)  # input index of each leaf (grad output order)
         nodes = _input_nodes(ctx, inputs)
         gauss = (means3D, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
@@ -422,13 +436,15 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         rs = raster_settings
         empty = torch.empty(0, device=means.device)
         ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)  # a backward can follow
+        info = {}
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians(
             rs.bg, means, colors, opacity_logits, log_scales, quaternions, rs.scale_modifier, empty,
             rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
             rs.sh_degree, rs.campos, rs.prefiltered, activations=_C.ACT_ALL,
-            prepare_backward=ctx.prep)
+            prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info)
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
+        ctx.binning_layout = info["binning_layout"]
         ctx.opacity_shape = opacity_logits.shape
         ctx.leaves = (means2D, colors, opacity_logits, means, None, sh, log_scales, quaternions)
         ctx.tensor_pos = _tensor_positions((means, means2D, sh, colors, opacity_logits, log_scales, quaternions))
@@ -456,7 +472,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                           rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                           rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,
                           rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                          activations=_C.ACT_ALL, prepare_backward=ctx.prep)):
+                          activations=_C.ACT_ALL, prepare_backward=ctx.prep, binning_layout=ctx.binning_layout)):
             return (None,) * 9
         acc = [_accumulation_target(t, node) if i is not None and need[i] else None
                for t, i, node in zip(ctx.leaves, inputs, nodes)]
@@ -469,7 +485,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
                 rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
                 activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc, prepare_backward=ctx.prep,
-                needed=needed)
+                needed=needed, binning_layout=ctx.binning_layout)
         done = [t is not None or not n for t, n in zip(acc, needed)]  # in the leaf's .grad / not needed: None
         return (None if done[3] else g_means, None if (done[0] or not need[1]) else g_means2D,
                 None if (done[5] or not sh.numel()) else g_sh,

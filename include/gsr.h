@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 13
+#define GSR_ABI_VERSION 14
 
 enum gsr_status {
     GSR_OK = 0,
@@ -106,6 +106,10 @@ typedef struct gsr_gaussians {
      * in gsr_backward_items_bytes() extra bytes at the end of the BINNING buffer.  gsr_backward /
      * gsr_backward_render: must equal the value the forward was called with. */
     int prepare_backward;
+    /* ABI >= 14.  gsr_backward / gsr_backward_render: the BINNING layout the forward reported
+     * (gsr_forward_info.binning_layout); 0 = num_rendered (gsr_forward, or a forward that did not
+     * enqueue speculatively).  Ignored by the forward. */
+    int binning_layout;
 } gsr_gaussians;
 
 /* Bits of gsr_grads.accumulate (ABI >= 6), one per output array. */
@@ -143,6 +147,28 @@ typedef struct gsr_grads {
 int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
                 float *out_color, float *out_depth, int *out_radii, int *out_num_rendered,
                 void *stream);
+
+/* Speculative enqueue (ABI >= 14).  gsr_forward waits on the host for num_rendered between the
+ * tile-count scan and the pair emission (the BINNING buffer is sized by it), so the stream idles while
+ * the host reads K back, calls the allocator and launches the rest.  gsr_forward_info_call with
+ * `speculate` set queues the post-scan kernels BEFORE that read-back, against a BINNING capacity of
+ * 1.25 x the largest pair count seen for this (device, P, W, H) + 65536 (no speculation on a first
+ * call, or when the last one needed the long-list merge sort); k_bin_scan checks the capacity on the
+ * device and those kernels return at once when it fails, in which case the host redoes them with the
+ * exact count before returning -- the outputs are the same either way (bitwise).  The call still
+ * returns after num_rendered is known.  `info->binning_layout` is the pair count the BINNING buffer
+ * is laid out for (the capacity, or num_rendered); pass it to the backward calls in
+ * gsr_gaussians.binning_layout and to gsr_buffer_offsets. */
+typedef struct gsr_forward_info {
+    int num_rendered;    /* K, the reference's num_rendered */
+    int binning_layout;  /* the pair count BINNING is laid out for (>= num_rendered) */
+    int speculated;      /* 1: the speculatively queued kernels stood; 0: exact path */
+} gsr_forward_info;
+int gsr_forward_info_call(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                          float *out_color, float *out_depth, int *out_radii, int speculate, gsr_forward_info *info,
+                          void *stream);
+/* Speculation counters since the last reset (stood / redone); reset != 0 also clears the history. */
+int gsr_spec_stats(int *hits, int *misses, int reset);
 
 /* Backward of gsr_forward given dL/d(color) (3,H,W).  dL_ddepth is accepted and ignored: the
  * reference discards the depth output (train.py:355-361, densify.py:120-126) and its -w-depth

@@ -1,7 +1,9 @@
 """Kernel concurrency over a rocprofv3 kernel trace window (several streams, one GPU).
 
-usage: python tools/concurrency_profile.py <trace_dir> [--frac F]
-Over the last FRAC of the trace: the share of wall time with 0, 1, 2, 3, 4+ kernels in flight, and
+usage: python tools/concurrency_profile.py <trace_dir> [--frac F] [--window K0:A:K1:B]
+Over the last FRAC of the trace (or from the start of launch A of kernel K0 to the end of launch B of
+kernel K1, e.g. k_preprocess:40:k_gauss_bwd_multi:27 = bench.py's timed region at warmup 5, probe 3,
+20 steps): the share of wall time with 0, 1, 2, 3, 4+ kernels in flight, and
 per kernel name its summed duration, its duration while running alone, and the mean number of
 other kernels in flight beside it -- which kernels share the chip and which run exposed."""
 import argparse
@@ -21,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
     ap.add_argument("--frac", type=float, default=0.2)
+    ap.add_argument("--window", default=None)
     a = ap.parse_args()
     rows = []
     for f in glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True):
@@ -28,8 +31,14 @@ def main():
             for r in csv.DictReader(fh):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), _short(r["Kernel_Name"])))
     rows.sort()
-    t0 = rows[0][0] + (1 - a.frac) * (rows[-1][1] - rows[0][0])
-    rows = [r for r in rows if r[0] >= t0]
+    if a.window:
+        k0, i0, k1, i1 = a.window.split(":")
+        t0 = [r for r in rows if r[2] == k0][int(i0)][0]
+        tend = [r for r in rows if r[2] == k1][int(i1)][1]
+        rows = [r for r in rows if r[0] >= t0 and r[1] <= tend]
+    else:
+        t0 = rows[0][0] + (1 - a.frac) * (rows[-1][1] - rows[0][0])
+        rows = [r for r in rows if r[0] >= t0]
     t1 = max(e for _, e, _ in rows)
     ev = []
     for i, (s, e, n) in enumerate(rows):
