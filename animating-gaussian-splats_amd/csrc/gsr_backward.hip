@@ -641,6 +641,32 @@ template <int MC> constexpr int kRecStageF4 = 3 * kRecChunk<MC>;  // float4 per 
 // A chunk of n packed records starting at record cb, as lane-contiguous float4 loads from the
 // 16-byte aligned address at or below its first float: (kRecF cb) & 3 floats of lead-in.
 __host__ __device__ constexpr int rec_chunk_f4(int C) { return (kRecF * C + 3 + 3) / 4; }
+// A lane's records [lo, hi) of a chunk staged at `sf` (record cb at sf[0]), added into acc in
+// emission order.  GSR_REC_UNROLL records per trip with their LDS reads issued together; past hi the
+// slots read as -0, the exact identity of fp32 addition, so the sums are bitwise those of a
+// one-record-per-trip walk (2 and 4 per trip measured slower: DESIGN 2.5).
+#ifndef GSR_REC_UNROLL
+#define GSR_REC_UNROLL 1
+#endif
+__device__ inline void add_chunk_records(const float *sf, uint32_t cb, uint32_t lo, uint32_t hi,
+                                         float (&acc)[kPartial]) {
+    constexpr int U = GSR_REC_UNROLL;
+    for (uint32_t e = lo; e < hi; e += U) {
+        float r[U][kPartial];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float *p = sf + kRecF * (e + u - cb);
+            const bool in = U == 1 || e + u < hi;
+#pragma unroll
+            for (int k = 0; k < kPartial; ++k) r[u][k] = in ? p[k] : -0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < kPartial; ++k) acc[k] += r[u][k];
+    }
+}
+
 template <int C>  // records per staged chunk (the wave's LDS slice holds 3 C float4)
 __device__ inline void sum_records_span(uint32_t e0, uint32_t e1, const float4 *__restrict__ part,
                                         float4 *stage, float (&acc)[kPartial]) {
@@ -666,12 +692,7 @@ __device__ inline void sum_records_span(uint32_t e0, uint32_t e1, const float4 *
             stage[lane + 64 * t] = v[t];  // a predicated store would sink its load into the branch
         wave_lds_sync();
         const float *sf = reinterpret_cast<const float *>(stage) + lead;
-        const uint32_t a = max(e0, cb), b = min(e1, cb + C);
-        for (uint32_t e = a; e < b; ++e) {
-            const float *r = sf + kRecF * (e - cb);
-#pragma unroll
-            for (int k = 0; k < kPartial; ++k) acc[k] += r[k];
-        }
+        add_chunk_records(sf, cb, max(e0, cb), min(e1, cb + C), acc);
         wave_lds_sync();
     }
 }
@@ -712,26 +733,23 @@ __device__ inline void view_chain(float3 mean, const float (&c3)[6], const float
     const m3 c2 = m3_mul(m3_mul(m3_T(T), m3_T(V)), T);
     const float a = GM(c2, 0, 0) + 0.3f, b = GM(c2, 0, 1), c = GM(c2, 1, 1) + 0.3f;
     const float denom = a * c - b * b;
-    float dL_da = 0, dL_db = 0, dL_dc = 0;
+    // upstream: every term zero when the determinant's inverse square vanishes; selects instead of a
+    // branch (a branch merging the six sums kept them in scratch memory)
     const float inv_det2 = 1.0f / ((denom * denom) + 0.0000001f);
+    const bool live = inv_det2 != 0;
+    const float dL_da = live ? inv_det2 * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz) : 0.f;
+    const float dL_dc = live ? inv_det2 * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx) : 0.f;
+    const float dL_db = live ? inv_det2 * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz) : 0.f;
 #define TT(cc, rr) GM(T, cc, rr)
-    if (inv_det2 != 0) {
-        dL_da = inv_det2 * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
-        dL_dc = inv_det2 * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
-        dL_db = inv_det2 * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
-        dcov[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
-        dcov[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
-        dcov[5] = (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc);
-        dcov[1] = 2 * TT(0, 0) * TT(0, 1) * dL_da + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dL_db +
-                  2 * TT(1, 0) * TT(1, 1) * dL_dc;
-        dcov[2] = 2 * TT(0, 0) * TT(0, 2) * dL_da + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dL_db +
-                  2 * TT(1, 0) * TT(1, 2) * dL_dc;
-        dcov[4] = 2 * TT(0, 2) * TT(0, 1) * dL_da + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dL_db +
-                  2 * TT(1, 1) * TT(1, 2) * dL_dc;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dcov[k] = 0;
-    }
+    dcov[0] = live ? (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc) : 0.f;
+    dcov[3] = live ? (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc) : 0.f;
+    dcov[5] = live ? (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc) : 0.f;
+    dcov[1] = live ? 2 * TT(0, 0) * TT(0, 1) * dL_da + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dL_db +
+                         2 * TT(1, 0) * TT(1, 1) * dL_dc : 0.f;
+    dcov[2] = live ? 2 * TT(0, 0) * TT(0, 2) * dL_da + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dL_db +
+                         2 * TT(1, 0) * TT(1, 2) * dL_dc : 0.f;
+    dcov[4] = live ? 2 * TT(0, 2) * TT(0, 1) * dL_da + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dL_db +
+                         2 * TT(1, 1) * TT(1, 2) * dL_dc : 0.f;
 #define VV(cc, rr) GM(V, cc, rr)
     const float dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
                        (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_db;
@@ -862,14 +880,14 @@ __device__ inline void gauss_bwd_one(
     if (MC > 0) {
         bool cl[3];
         const float3 cp = load_campos(campos, cs.c0);
-        (void)sh_to_rgb(D, mean, cp, s_row, cl);  // recompute the forward's clamp mask
+        clamp_from_rec(rec, i, cl);  // the forward's clamp mask
         const float3 d = sh_backward(D, MC, mean, cp, s_row, cl, make_float3(acc[6], acc[7], acc[8]), s_row);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
     } else if (shs) {
         const float *sh = shs + (size_t)i * M * 3;
         bool cl[3];
         const float3 cp = load_campos(campos, cs.c0);
-        (void)sh_to_rgb(D, mean, cp, sh, cl);
+        clamp_from_rec(rec, i, cl);
         const float3 d = sh_backward(D, M, mean, cp, sh, cl, make_float3(acc[6], acc[7], acc[8]),
                                      dL_dsh ? dL_dsh + (size_t)i * M * 3 : nullptr, ash);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
@@ -954,6 +972,9 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
 constexpr int kMultiChunk = 128;  // records per staged chunk (36 B each, per wave)
 constexpr int kMultiStageF4 = 5 * 64;  // float4 of a wave's staged chunk (RecChunk): 5 KB of LDS
+#ifndef GSR_MV_NOREC
+#define GSR_MV_NOREC 0
+#endif
 #ifndef GSR_MV_WPE
 #define GSR_MV_WPE 0  // waves per SIMD the register budget is held to (0: the compiler's choice)
 #endif
@@ -1050,6 +1071,11 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         float acc[kPartial];
 #pragma unroll
         for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
+#if GSR_MV_NOREC  // diagnostic: no record walk (timing of the rest of the pass)
+        acc[0] = (float)e0 * 1e-9f; acc[1] = (float)e1 * 1e-9f;
+        (void)have; (void)lane; (void)buf;
+        if (false) {
+#endif
         const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0), E1 = __builtin_amdgcn_readlane(e1, 63);
         if (E0 < E1 && !have) buf = mv_load(V.part, E0, E1, lane);
         for (uint32_t cb = E0; cb < E1; cb += kMultiChunk) {  // wave-collective
@@ -1067,15 +1093,13 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
                 }
             }
             wave_lds_sync();
-            const uint32_t lo = max(e0, cb), hi = min(e1, cb + kMultiChunk);
             const float *sf = reinterpret_cast<const float *>(stage) + ((kRecF * cb) & 3u);
-            for (uint32_t e = lo; e < hi; ++e) {
-                const float *r = sf + kRecF * (e - cb);
-#pragma unroll
-                for (int k = 0; k < kPartial; ++k) acc[k] += r[k];
-            }
+            add_chunk_records(sf, cb, max(e0, cb), min(e1, cb + kMultiChunk), acc);
             wave_lds_sync();
         }
+#if GSR_MV_NOREC
+        }
+#endif
         if (!live) continue;
         const bool r = rv > 0;
         if (V.dL_dmeans2D) {
@@ -1108,7 +1132,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if constexpr (MC > 0) {
             const float3 cp = load_campos(V.campos, V.cs.c0);
             bool cl[3];
-            (void)sh_to_rgb(a.D, mean, cp, s_row, cl);  // the forward's clamp mask in this view
+            clamp_from_rec(V.rec, i, cl);  // the forward's clamp mask in this view
             const float3 d0 = make_float3(mean.x - cp.x, mean.y - cp.y, mean.z - cp.z);
             const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
             const float x = d0.x / len, y = d0.y / len, z = d0.z / len;

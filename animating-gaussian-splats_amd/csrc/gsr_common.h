@@ -445,6 +445,17 @@ __device__ inline float3 sh_to_rgb(int deg, float3 mean, float3 campos, ShPtr sh
     return make_float3(out[0], out[1], out[2]);
 }
 
+// The forward's SH clamp mask (bit c: channel c's colour was clamped at 0) rides in the otherwise
+// unused .w of the render record's colour slot (rec[2]), so the backward reads it instead of
+// re-evaluating the SH colour in every view.
+__device__ inline float clamp_bits(const bool (&cl)[3]) {
+    return __uint_as_float((cl[0] ? 1u : 0u) | (cl[1] ? 2u : 0u) | (cl[2] ? 4u : 0u));
+}
+__device__ inline void clamp_from_rec(const float4 *__restrict__ rec, size_t i, bool (&cl)[3]) {
+    const uint32_t m = __float_as_uint(rec[(size_t)kRecF4 * i + 2].w);
+    cl[0] = m & 1u; cl[1] = m & 2u; cl[2] = m & 4u;
+}
+
 // rect packing: x = x0 | y0 << 16, y = x1 | y1 << 16
 __device__ inline uint2 pack_rect(int x0, int y0, int x1, int y1) {
     return make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));

@@ -107,6 +107,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     get_rect(pix_x, pix_y, (int)my_radius, gx, gy, x0, y0, x1, y1);
     if ((x1 - x0) * (y1 - y0) == 0) return;
     float3 rgb;
+    float clm = 0.f;  // the SH clamp mask for the backward (clamp_bits)
     if (colors_precomp) {
         rgb = make_float3(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2]);
     } else {
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
         const float3 cp = load_campos(campos, cs.c0);
         if (MC > 0) rgb = sh_to_rgb(D, p, cp, s_sh + threadIdx.x * RS, cl);
         else rgb = sh_to_rgb(D, p, cp, shs + (size_t)i * M * 3, cl);
+        clm = clamp_bits(cl);
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
@@ -123,7 +125,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     float4 *r = rec_out + (size_t)kRecF4 * i;
     r[0] = make_float4(pix_x, pix_y, -0.5f * GSR_LOG2E * ca, -GSR_LOG2E * cb);
     r[1] = make_float4(-0.5f * GSR_LOG2E * cc, o, pv.z, tau2);
-    r[2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+    r[2] = make_float4(rgb.x, rgb.y, rgb.z, clm);
     r[3] = make_float4(ca, cb, cc, 0.f);
     rect_out[i] = pack_rect(x0, y0, x1, y1);
     tiles_out[i] = (uint32_t)((y1 - y0) * (x1 - x0));

@@ -53,23 +53,25 @@ def test_speculative_forward_is_bitwise_the_exact_path(cuda):
     a = {k: v for k, v in S.activated_inputs(S.synthetic_cloud(P, 0.01, sh_degree=3, seed=21, device=cuda), 3).items()
          if k != "means2D" and v is not None}
     a.pop("colors_precomp", None)
-    far = S.render_settings(W, H, S.intrinsics(500.0, W, H), S.look_at(30, 0.2, 9.0), device=cuda, sh_degree=3)
-    near = S.render_settings(W, H, S.intrinsics(500.0, W, H), S.look_at(30, 0.2, 3.0), device=cuda, sh_degree=3)
+    # the same (P, W, H) key twice: the cloud as is, and with 4x the scales (each Gaussian covers more
+    # tiles: K 111873 -> 256884 by the CPU oracle, longest list 2488, no merge sort)
+    cam = S.render_settings(W, H, S.intrinsics(500.0, W, H), S.look_at(30, 0.2, 9.0), device=cuda, sh_degree=3)
+    dense = dict(a, scales=a["scales"] * 4.0)
     dl = S.upstream_grad(H, W, device=cuda)
     _C.speculation_stats(reset=True)
-    exact_far = _render(a, far, False, dl)
+    exact_far = _render(a, cam, False, dl)
     assert exact_far[0]["speculated"] is False and exact_far[0]["binning_layout"] == exact_far[0]["num_rendered"]
-    first = _render(a, far, True, dl)       # history from the exact call above: speculates
+    first = _render(a, cam, True, dl)       # history from the exact call above: speculates
     assert first[0]["speculated"] and first[0]["binning_layout"] > first[0]["num_rendered"]
     _same(first, exact_far)
-    exact_near = _render(a, near, False, dl)
+    exact_near = _render(dense, cam, False, dl)
     _C.speculation_stats(reset=True)
-    _render(a, far, False, dl)               # history: the sparse far view only
-    grown = _render(a, near, True, dl)       # K well above 1.25 x the history: redone exactly
+    _render(a, cam, False, dl)               # history: the sparse cloud only
+    grown = _render(dense, cam, True, dl)    # K well above 1.25 x the history: redone exactly
     assert exact_near[0]["num_rendered"] > 1.3 * exact_far[0]["num_rendered"] + 65536
     assert grown[0]["speculated"] is False
     _same(grown, exact_near)
-    again = _render(a, near, True, dl)       # history now holds the dense view: stands
+    again = _render(dense, cam, True, dl)    # history now holds the dense cloud: stands
     assert again[0]["speculated"]
     _same(again, exact_near)
     hits, misses = _C.speculation_stats()
@@ -91,8 +93,9 @@ def test_speculation_falls_back_on_long_lists(cuda):
     rs = S.render_settings(64, 64, S.intrinsics(64.0, 64, 64), S.look_at(0, 0, 4), device=cuda)
     dl = S.upstream_grad(64, 64, device=cuda)
     exact = _render(a, rs, False, dl)
-    # seed a history without long lists for this (P, W, H): the same cloud spread out
-    spread = dict(a, means3D=a["means3D"] * torch.tensor([100.0, 100.0, 1.0], device=cuda))
+    # seed a history without long lists for this (P, W, H): the same cloud spread out (x300: K 9307,
+    # longest list 641 by the CPU oracle; x100 still leaves a 4186-pair tile)
+    spread = dict(a, means3D=a["means3D"] * torch.tensor([300.0, 300.0, 1.0], device=cuda))
     _C.speculation_stats(reset=True)
     _render(spread, rs, False, dl)
     got = _render(a, rs, True, dl)
