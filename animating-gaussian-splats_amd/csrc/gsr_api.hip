@@ -217,6 +217,7 @@ void carve_geom(FwdArgs &a, char *base) {
     const GeomLayout L(a.P);
     a.depth = (float *)(base + L.depth); a.rec = (float4 *)(base + L.rec);
     a.rect = (uint2 *)(base + L.rect); a.tiles = (uint32_t *)(base + L.tiles); a.goff = (uint32_t *)(base + L.goff);
+    a.clampm = (uint8_t *)(base + L.clampm);
 }
 void carve_image(FwdArgs &a, char *base) {
     const ImageLayout L(a.W, a.H, a.P);
@@ -472,7 +473,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.colors_precomp = f.colors_precomp; a.cov3D_precomp = f.cov3D_precomp;
     a.viewmatrix = f.viewmatrix; a.projmatrix = f.projmatrix; a.campos = f.campos; a.bg = f.bg; a.cs = f.cs;
     a.radii = radii;
-    a.rec = f.rec; a.rect = f.rect; a.goff = f.goff;
+    a.rec = f.rec; a.rect = f.rect; a.goff = f.goff; a.clampm = f.clampm;
     a.ranges = f.ranges; a.pix_end = f.pix_end; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
     a.seg_off = f.seg_off; a.meta = f.meta;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
@@ -575,6 +576,7 @@ int gsr_backward_gaussians(int nviews, const gsr_view_grad *views, const gsr_gau
             mv.radii = vg.radii;
             mv.goff = (const uint32_t *)((const char *)vg.geom + GeomLayout(g->P).goff);
             mv.rec = (const float4 *)((const char *)vg.geom + GeomLayout(g->P).rec);
+            mv.clampm = (const uint8_t *)vg.geom + GeomLayout(g->P).clampm;
             mv.part = (const float4 *)((const char *)vg.scratch +
                                        ScratchLayout(vg.num_rendered, f.gx * f.gy).part);
             mv.dL_dmeans2D = vg.dL_dmeans2D;

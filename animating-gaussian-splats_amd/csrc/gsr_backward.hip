@@ -800,7 +800,8 @@ __device__ inline void gauss_bwd_one(
     const int *__restrict__ radii, const float (&acc)[kPartial], float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec, int accm) {
+    float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec, int accm,
+    const uint8_t *__restrict__ clampm) {
     // every output may be NULL (gradient not requested: the input does not require grad); accm:
     // gsr_grad_bits of the outputs to add into instead of overwrite
     const bool a2 = accm & GSR_GRAD_MEANS2D, ac = accm & GSR_GRAD_COLORS, ao = accm & GSR_GRAD_OPACITY,
@@ -880,14 +881,14 @@ __device__ inline void gauss_bwd_one(
     if (MC > 0) {
         bool cl[3];
         const float3 cp = load_campos(campos, cs.c0);
-        clamp_from_rec(rec, i, cl);  // the forward's clamp mask
+        clamp_from_mask(clampm[i], cl);  // the forward's clamp mask
         const float3 d = sh_backward(D, MC, mean, cp, s_row, cl, make_float3(acc[6], acc[7], acc[8]), s_row);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
     } else if (shs) {
         const float *sh = shs + (size_t)i * M * 3;
         bool cl[3];
         const float3 cp = load_campos(campos, cs.c0);
-        clamp_from_rec(rec, i, cl);
+        clamp_from_mask(clampm[i], cl);
         const float3 d = sh_backward(D, M, mean, cp, sh, cl, make_float3(acc[6], acc[7], acc[8]),
                                      dL_dsh ? dL_dsh + (size_t)i * M * 3 : nullptr, ash);
         dm0 += d.x; dm1 += d.y; dm2 += d.z;
@@ -933,7 +934,8 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     const float4 *__restrict__ part, float *__restrict__ dL_dmeans2D,
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
-    float *__restrict__ dL_drot, int act, const float4 *__restrict__ rec, int accm) {
+    float *__restrict__ dL_drot, int act, const float4 *__restrict__ rec, int accm,
+    const uint8_t *__restrict__ clampm) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
@@ -951,7 +953,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
                                  scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos, cs,
                                  radii, acc, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
-                                 act, rec, accm);
+                                 act, rec, accm, clampm);
     if constexpr (MC > 0) {  // coalesced store of the dL/dSH rows
         if (!dL_dsh) return;
         __syncthreads();
@@ -1132,7 +1134,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if constexpr (MC > 0) {
             const float3 cp = load_campos(V.campos, V.cs.c0);
             bool cl[3];
-            clamp_from_rec(V.rec, i, cl);  // the forward's clamp mask in this view
+            clamp_from_mask(V.clampm[i], cl);  // the forward's clamp mask in this view
             const float3 d0 = make_float3(mean.x - cp.x, mean.y - cp.y, mean.z - cp.z);
             const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
             const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
@@ -1260,7 +1262,7 @@ static void gauss_bwd_mc(const BwdArgs &a, hipStream_t s) {
         a.P, a.D, a.M, a.W, a.H, a.scale_modifier, a.tan_fovx, a.tan_fovy, a.focal_x, a.focal_y,
         a.means3D, a.scales, a.rotations, a.shs, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.cs,
         a.radii, a.goff, a.part, a.dL_dmeans2D, a.dL_dcolors, a.dL_dopacity,
-        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot, a.act, a.rec, a.accm);
+        a.dL_dmeans3D, a.dL_dcov3D, a.dL_dsh, a.dL_dscales, a.dL_drot, a.act, a.rec, a.accm, a.clampm);
 }
 
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {

@@ -42,7 +42,7 @@ __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_
 //   depth/rect/tiles/goff: SoA arrays for the binning kernels.
 constexpr int kRecF4 = 4;  // float4 per render record (64 B)
 struct GeomLayout {
-    size_t depth, rec, rect, tiles, goff, total;
+    size_t depth, rec, rect, tiles, goff, clampm, total;
     __host__ __device__ GeomLayout(int P) {
         size_t o = 0;
         depth = o;    o = align256(o + sizeof(float) * P);
@@ -50,6 +50,7 @@ struct GeomLayout {
         rect = o;     o = align256(o + sizeof(uint2) * P);
         tiles = o;    o = align256(o + sizeof(uint32_t) * P);
         goff = o;     o = align256(o + sizeof(uint32_t) * (P + 1));
+        clampm = o;   o = align256(o + (size_t)P);  // SH clamp mask per Gaussian (clamp_bits)
         total = o;
     }
 };
@@ -445,16 +446,12 @@ __device__ inline float3 sh_to_rgb(int deg, float3 mean, float3 campos, ShPtr sh
     return make_float3(out[0], out[1], out[2]);
 }
 
-// The forward's SH clamp mask (bit c: channel c's colour was clamped at 0) rides in the otherwise
-// unused .w of the render record's colour slot (rec[2]), so the backward reads it instead of
-// re-evaluating the SH colour in every view.
-__device__ inline float clamp_bits(const bool (&cl)[3]) {
-    return __uint_as_float((cl[0] ? 1u : 0u) | (cl[1] ? 2u : 0u) | (cl[2] ? 4u : 0u));
+// The forward's SH clamp mask (bit c: channel c's colour was clamped at 0), one byte per Gaussian in
+// GEOM (`clampm`): the backward reads it instead of re-evaluating the SH colour in every view.
+__device__ inline uint8_t clamp_bits(const bool (&cl)[3]) {
+    return (uint8_t)((cl[0] ? 1u : 0u) | (cl[1] ? 2u : 0u) | (cl[2] ? 4u : 0u));
 }
-__device__ inline void clamp_from_rec(const float4 *__restrict__ rec, size_t i, bool (&cl)[3]) {
-    const uint32_t m = __float_as_uint(rec[(size_t)kRecF4 * i + 2].w);
-    cl[0] = m & 1u; cl[1] = m & 2u; cl[2] = m & 4u;
-}
+__device__ inline void clamp_from_mask(uint32_t m, bool (&cl)[3]) { cl[0] = m & 1u; cl[1] = m & 2u; cl[2] = m & 4u; }
 
 // rect packing: x = x0 | y0 << 16, y = x1 | y1 << 16
 __device__ inline uint2 pack_rect(int x0, int y0, int x1, int y1) {

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     float tan_fovx, float tan_fovy, float focal_x, float focal_y, int gx, int gy,
     int *__restrict__ radii, float *__restrict__ depth_out, float4 *__restrict__ rec_out,
     uint2 *__restrict__ rect_out, uint32_t *__restrict__ tiles_out, int act, CamStrides cs,
-    uint32_t *__restrict__ tile_count, int T) {
+    uint32_t *__restrict__ tile_count, int T, uint8_t *__restrict__ clamp_out) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
     const int i0 = blockIdx.x * kShBlock;
@@ -107,7 +107,6 @@ __global__ __launch_bounds__(256) void k_preprocess(
     get_rect(pix_x, pix_y, (int)my_radius, gx, gy, x0, y0, x1, y1);
     if ((x1 - x0) * (y1 - y0) == 0) return;
     float3 rgb;
-    float clm = 0.f;  // the SH clamp mask for the backward (clamp_bits)
     if (colors_precomp) {
         rgb = make_float3(colors_precomp[3 * i], colors_precomp[3 * i + 1], colors_precomp[3 * i + 2]);
     } else {
@@ -115,7 +114,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
         const float3 cp = load_campos(campos, cs.c0);
         if (MC > 0) rgb = sh_to_rgb(D, p, cp, s_sh + threadIdx.x * RS, cl);
         else rgb = sh_to_rgb(D, p, cp, shs + (size_t)i * M * 3, cl);
-        clm = clamp_bits(cl);
+        clamp_out[i] = clamp_bits(cl);  // for the backward's SH chain
     }
     radii[i] = (int)my_radius;
     depth_out[i] = pv.z;
@@ -125,7 +124,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     float4 *r = rec_out + (size_t)kRecF4 * i;
     r[0] = make_float4(pix_x, pix_y, -0.5f * GSR_LOG2E * ca, -GSR_LOG2E * cb);
     r[1] = make_float4(-0.5f * GSR_LOG2E * cc, o, pv.z, tau2);
-    r[2] = make_float4(rgb.x, rgb.y, rgb.z, clm);
+    r[2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
     r[3] = make_float4(ca, cb, cc, 0.f);
     rect_out[i] = pack_rect(x0, y0, x1, y1);
     tiles_out[i] = (uint32_t)((y1 - y0) * (x1 - x0));
@@ -894,7 +893,7 @@ static void preprocess_mc(const FwdArgs &a, hipStream_t s) {
         a.P, a.D, a.M, a.means3D, a.scales, a.scale_modifier, a.rotations, a.opacities, a.shs,
         a.colors_precomp, a.cov3D_precomp, a.viewmatrix, a.projmatrix, a.campos, a.W, a.H, a.tan_fovx,
         a.tan_fovy, a.focal_x, a.focal_y, a.gx, a.gy, a.radii, a.depth, a.rec, a.rect, a.tiles, a.act, a.cs,
-        a.tile_count, a.gx * a.gy);
+        a.tile_count, a.gx * a.gy, a.clampm);
 }
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s) {

@@ -13,7 +13,7 @@ struct FwdArgs {
     const float *viewmatrix, *projmatrix, *campos, *bg;
     CamStrides cs;
     // geom
-    float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff;
+    float *depth; float4 *rec; uint2 *rect; uint32_t *tiles; uint32_t *goff; uint8_t *clampm;
     // image
     uint2 *ranges; float4 *pix_end; uint32_t *n_contrib; uint32_t *tile_maxc;
     uint32_t *tile_order_f; uint32_t *seg_off; uint32_t *sort_lists; uint32_t *tile_count;
@@ -38,7 +38,7 @@ struct BwdArgs {
     CamStrides cs;
     const int *radii;
     // saved state
-    const float4 *rec; const uint2 *rect;
+    const float4 *rec; const uint2 *rect; const uint8_t *clampm;
     const uint32_t *goff; const uint2 *ranges; const float4 *pix_end; const uint32_t *n_contrib;
     const uint32_t *tile_maxc; const uint32_t *seg_off; const uint32_t *meta;
     const uint32_t *point_list; const uint32_t *slot_emit; const float4 *seg_state;
@@ -80,6 +80,7 @@ struct MultiView {
     const int *radii;
     const uint32_t *goff;   // the view's emission offsets (GEOM)
     const float4 *rec;      // the view's render records (GEOM): the activated opacity (sigmoid chain)
+    const uint8_t *clampm;  // the view's SH clamp masks (GEOM)
     const float4 *part;     // the view's per-pair records (SCRATCH, gsr_backward_render)
     float *dL_dmeans2D;     // the view's screen-space gradient (P,3) or NULL
     int acc2;               // add into dL_dmeans2D instead of overwriting
