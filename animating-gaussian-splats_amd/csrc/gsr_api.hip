@@ -251,6 +251,7 @@ size_t gsr_binning_bytes(int K) { return BinningLayout(K).total; }
 size_t gsr_backward_items_bytes(int K, int W, int H) {
     return bwd_items_bytes(K < 0 ? 0 : K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH));
 }
+size_t gsr_sums_bytes(int P) { return align256(sizeof(float) * kPartial * (size_t)(P < 0 ? 0 : P)); }
 size_t gsr_scratch_bytes(int K, int W, int H) {
     return ScratchLayout(K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH)).total;
 }
@@ -452,7 +453,7 @@ namespace {
 // buffer (records at a.part) requested through `alloc`.
 int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *radii, int num_rendered,
                     const void *geom, const void *binning, const void *image, const float *dL_dcolor,
-                    gsr_alloc_fn alloc, void *alloc_ctx, hipStream_t s, BwdArgs &a) {
+                    gsr_alloc_fn alloc, void *alloc_ctx, hipStream_t s, BwdArgs &a, bool sums = false) {
     if (!geom || !binning || !image || !dL_dcolor || !radii || !alloc)
         return fail(GSR_ERR_ARG, "gsr_backward: missing saved buffers / dL_dcolor / allocator");
     if (num_rendered < 0) return fail(GSR_ERR_ARG, "num_rendered < 0");
@@ -491,6 +492,12 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
         HIP_TRY(launch_bwd_items(a, s));
     }
     { Phase ph(s, "render_bwd"); HIP_TRY(launch_render_bwd(a, s)); }
+    if (sums) {  // deferred view: its per-Gaussian record sums for gsr_backward_gaussians (SUMS buffer)
+        float *out = (float *)alloc(alloc_ctx, GSR_BUF_SUMS, gsr_sums_bytes(a.P));
+        if (!out) return fail(GSR_ERR_ALLOC, "allocation callback failed (sums)");
+        Phase ph(s, "sum_records");
+        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s));
+    }
     return GSR_OK;
 }
 }  // namespace
@@ -531,7 +538,7 @@ int gsr_backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int
     if (g->P == 0) return GSR_OK;
     BwdArgs a;
     return backward_render(cam, g, radii, num_rendered, geom, binning, image, dL_dcolor, alloc, alloc_ctx,
-                           (hipStream_t)stream, a);
+                           (hipStream_t)stream, a, true);
 }
 
 int gsr_backward_gaussians(int nviews, const gsr_view_grad *views, const gsr_gaussians *g, gsr_grads *out,
@@ -574,11 +581,9 @@ int gsr_backward_gaussians(int nviews, const gsr_view_grad *views, const gsr_gau
             mv.cs = f.cs;
             mv.tan_fovx = f.tan_fovx; mv.tan_fovy = f.tan_fovy; mv.focal_x = f.focal_x; mv.focal_y = f.focal_y;
             mv.radii = vg.radii;
-            mv.goff = (const uint32_t *)((const char *)vg.geom + GeomLayout(g->P).goff);
             mv.rec = (const float4 *)((const char *)vg.geom + GeomLayout(g->P).rec);
             mv.clampm = (const uint8_t *)vg.geom + GeomLayout(g->P).clampm;
-            mv.part = (const float4 *)((const char *)vg.scratch +
-                                       ScratchLayout(vg.num_rendered, f.gx * f.gy).part);
+            mv.sums = (const float *)vg.scratch;  // the view's SUMS buffer (gsr_backward_render)
             mv.dL_dmeans2D = vg.dL_dmeans2D;
             mv.acc2 = vg.accumulate_means2D ? 1 : 0;
             written[7 + k] = vg.dL_dmeans2D;

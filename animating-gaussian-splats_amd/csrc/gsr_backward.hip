@@ -962,6 +962,26 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     }
 }
 
+// ---- per-view record sums (gsr_backward_render, deferred views) ---------------------------------
+// One thread per Gaussian, its wave's record span staged through LDS in 128-record chunks
+// (sum_records_span: lane-contiguous coalesced loads, each lane adding its own records in emission
+// order -- the same additions in the same order as k_gauss_bwd's walk), stored as kPartial x P SoA:
+// the multi-view pass then reads 9 coalesced words per Gaussian and view.  Few registers and 6 KB
+// of LDS per wave, so the walk's LDS round trips hide behind other waves; it runs on the view's
+// stream right after k_render_bwd, beside the other views' render kernels.
+constexpr int kSumChunk = 128;
+__global__ __launch_bounds__(256) void k_sum_records(int P, const uint32_t *__restrict__ goff,
+                                                     const float4 *__restrict__ part, float *__restrict__ sums) {
+    __shared__ float4 s_stage[3 * kSumChunk * 4];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    float acc[kPartial];
+    sum_records_chunked<kSumChunk>(i, P, goff, part, s_stage + (threadIdx.x >> 6) * 3 * kSumChunk, acc);
+    if (i < P) {
+#pragma unroll
+        for (int k = 0; k < kPartial; ++k) sums[(size_t)k * P + i] = acc[k];
+    }
+}
+
 // ---- the per-Gaussian backward of several views in one pass (gsr_backward_gaussians) -----------
 // A training step's views (train.py:753-767 sums 5 view losses before ONE backward) share every
 // parameter and gradient array: one thread per Gaussian reads its parameters and SH row once, walks
@@ -972,11 +992,6 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
 // read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
-constexpr int kMultiChunk = 128;  // records per staged chunk (36 B each, per wave)
-constexpr int kMultiStageF4 = 5 * 64;  // float4 of a wave's staged chunk (RecChunk): 5 KB of LDS
-#ifndef GSR_MV_NOREC
-#define GSR_MV_NOREC 0
-#endif
 #ifndef GSR_MV_WPE
 #define GSR_MV_WPE 0  // waves per SIMD the register budget is held to (0: the compiler's choice)
 #endif
@@ -988,32 +1003,12 @@ constexpr int kMultiStageF4 = 5 * 64;  // float4 of a wave's staged chunk (RecCh
 template <int MC>
 constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_stride(MC) + 3) & ~size_t(3)) : 0; }
 template <int MC>
-constexpr size_t multi_lds_bytes() {
-    return sizeof(float) * multi_sh_floats<MC>() + sizeof(float4) * kMultiStageF4 * (kShBlock / 64);
-}
-
-// The lane's share of one record chunk [cb, min(cb + 128, E1)): six float4 held in named registers
-// (an array live across the view loop's control flow stays in scratch memory).  Clamped index:
-// every load in bounds, none predicated.
-struct RecChunk { float4 b0, b1, b2, b3, b4; };
-static_assert(rec_chunk_f4(128) <= 5 * 64, "RecChunk holds a 128-record chunk");
-__device__ inline RecChunk mv_load(const float4 *__restrict__ part, uint32_t cb, uint32_t E1, int lane) {
-    const size_t f0 = (size_t)kRecF * cb;
-    const uint32_t lead = (uint32_t)(f0 & 3u);
-    const uint32_t nf4 = (lead + kRecF * min(128u, E1 - cb) + 3u) / 4u;
-    const float4 *src = reinterpret_cast<const float4 *>(reinterpret_cast<const float *>(part) + (f0 - lead));
-    RecChunk c;
-    c.b0 = src[min(lane + 0u, nf4 - 1u)];   c.b1 = src[min(lane + 64u, nf4 - 1u)];
-    c.b2 = src[min(lane + 128u, nf4 - 1u)]; c.b3 = src[min(lane + 192u, nf4 - 1u)];
-    c.b4 = src[min(lane + 256u, nf4 - 1u)];
-    return c;
-}
+constexpr size_t multi_lds_bytes() { return sizeof(float) * multi_sh_floats<MC>(); }
 
 template <int MC>  // SH coefficient count (1, 4, 9, 16), or 0 without SH (colours precomputed)
 __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const MultiArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     constexpr int RL = 3 * MC, RS = sh_row_stride(MC);
-    float4 *stage = reinterpret_cast<float4 *>(s_sh + multi_sh_floats<MC>()) + (threadIdx.x >> 6) * kMultiStageF4;
     const int P = a.P;
     const int i0 = blockIdx.x * kShBlock;
     const int nrow = min(kShBlock, P - i0);
@@ -1042,66 +1037,28 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     }
     float gm0 = 0.f, gm1 = 0.f, gm2 = 0.f, gop = 0.f, gc0 = 0.f, gc1 = 0.f, gc2 = 0.f;
     float gcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float gsh[RL > 0 ? RL : 1];
-#pragma unroll
-    for (int k = 0; k < (RL > 0 ? RL : 1); ++k) gsh[k] = 0.f;
     bool vis = false;
     float o_act = 0.f;  // the activated opacity, from the record of a view that sees the Gaussian
     float m2[3] = {0.f, 0.f, 0.f};  // the screen-space gradient carried across views of one array
     const int active = (a.D + 1) * (a.D + 1);
-    // each view's emission span and radius are loaded one view ahead (their latency then hides
-    // behind the previous view's records and chains instead of opening every view)
-    const int ic = min(i, P);
-    uint32_t e0n = a.v[0].goff[ic], e1n = a.v[0].goff[min(i + 1, P)];
+    // each view's record sums (gsr_backward_render's k_sum_records, kPartial x P SoA: coalesced) and
+    // radius are loaded one view ahead, so their latency hides behind the previous view's chains
+    float nx[kPartial];
+#pragma unroll
+    for (int k = 0; k < kPartial; ++k) nx[k] = a.v[0].sums[(size_t)k * P + ii];
     int rn = a.v[0].radii[ii];
-    // The records of all views stream through the wave's LDS slice in chunks of kMultiChunk, the
-    // loads of the next chunk -- of this view, or the next view's first -- in flight while the
-    // current chunk is summed and while a finished view's chains run (buf: 3 kMultiChunk / 64 float4
-    // per lane).  Same additions in the same order as sum_records_span.
-    static_assert(kMultiChunk == 128, "RecChunk holds 128 records");
-    const int lane = threadIdx.x & 63;
-    RecChunk buf = {};
-    bool have = false;  // buf holds (or is loading) the chunk the walk consumes next
     for (int v = 0; v < a.nv; ++v) {
         const MultiView &V = a.v[v];
-        const uint32_t e0 = e0n, e1 = e1n;
         const int rv = rn;
-        if (v + 1 < a.nv) {
-            const MultiView &Vn = a.v[v + 1];
-            e0n = Vn.goff[ic]; e1n = Vn.goff[min(i + 1, P)]; rn = Vn.radii[ii];
-        }
         float acc[kPartial];
 #pragma unroll
-        for (int k = 0; k < kPartial; ++k) acc[k] = 0.f;
-#if GSR_MV_NOREC  // diagnostic: no record walk (timing of the rest of the pass)
-        acc[0] = (float)e0 * 1e-9f; acc[1] = (float)e1 * 1e-9f;
-        (void)have; (void)lane; (void)buf;
-        if (false) {
-#endif
-        const uint32_t E0 = __builtin_amdgcn_readfirstlane(e0), E1 = __builtin_amdgcn_readlane(e1, 63);
-        if (E0 < E1 && !have) buf = mv_load(V.part, E0, E1, lane);
-        for (uint32_t cb = E0; cb < E1; cb += kMultiChunk) {  // wave-collective
-            stage[lane] = buf.b0; stage[lane + 64] = buf.b1; stage[lane + 128] = buf.b2;
-            stage[lane + 192] = buf.b3; stage[lane + 256] = buf.b4;
-            have = false;
-            if (cb + kMultiChunk < E1) {
-                buf = mv_load(V.part, cb + kMultiChunk, E1, lane);
-                have = true;
-            } else if (v + 1 < a.nv) {
-                const uint32_t E0n = __builtin_amdgcn_readfirstlane(e0n), E1n = __builtin_amdgcn_readlane(e1n, 63);
-                if (E0n < E1n) {
-                    buf = mv_load(a.v[v + 1].part, E0n, E1n, lane);
-                    have = true;
-                }
-            }
-            wave_lds_sync();
-            const float *sf = reinterpret_cast<const float *>(stage) + ((kRecF * cb) & 3u);
-            add_chunk_records(sf, cb, max(e0, cb), min(e1, cb + kMultiChunk), acc);
-            wave_lds_sync();
+        for (int k = 0; k < kPartial; ++k) acc[k] = nx[k];
+        if (v + 1 < a.nv) {
+            const MultiView &Vn = a.v[v + 1];
+#pragma unroll
+            for (int k = 0; k < kPartial; ++k) nx[k] = Vn.sums[(size_t)k * P + ii];
+            rn = Vn.radii[ii];
         }
-#if GSR_MV_NOREC
-        }
-#endif
         if (!live) continue;
         const bool r = rv > 0;
         if (V.dL_dmeans2D) {
@@ -1142,14 +1099,6 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
                                    acc[8] * (cl[2] ? 0.f : 1.f)};
             const float3 d = unit_vec_bwd(d0, sh_dir_grad(a.D, x, y, z, s_row, dRGB));
             dm0 += d.x; dm1 += d.y; dm2 += d.z;
-            float basis[16];
-            sh_basis16(x, y, z, basis);
-#pragma unroll
-            for (int k = 0; k < MC; ++k)
-                if (k < active) {
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) gsh[3 * k + c] += basis[k] * dRGB[c];
-                }
         }
         gm0 += dm0; gm1 += dm1; gm2 += dm2;
     }
@@ -1219,12 +1168,37 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             }
         }
     }
-    if constexpr (MC > 0) {  // the summed dL/dSH rows through LDS (over the coefficients), coalesced store
+    if constexpr (MC > 0) {
+        // dL/dSH = sum over the views of basis(dir_v) x dRGB_v, summed in the lane's own LDS row: the
+        // coefficients it held are no longer read (every view's direction gradient is done), and the
+        // 3 MC sums stay out of the registers the view loop needs (4 -> 3 waves/SIMD at SH3).  Same
+        // additions in the same order as running sums over the views.  dRGB_v is reloaded from the
+        // view's sums, the clamp mask and direction recomputed as in the loop.
         if (!a.dL_dsh) return;
-        __syncthreads();
         if (live) {
 #pragma unroll
-            for (int k = 0; k < RL; ++k) s_row[k] = gsh[k];
+            for (int k = 0; k < RL; ++k) s_row[k] = 0.f;
+            for (int v = 0; v < a.nv; ++v) {
+                const MultiView &V = a.v[v];
+                if (!(V.radii[i] > 0)) continue;
+                const float3 cp = load_campos(V.campos, V.cs.c0);
+                bool cl[3];
+                clamp_from_mask(V.clampm[i], cl);
+                const float3 d0 = make_float3(mean.x - cp.x, mean.y - cp.y, mean.z - cp.z);
+                const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
+                const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
+                const float dRGB[3] = {V.sums[(size_t)6 * P + i] * (cl[0] ? 0.f : 1.f),
+                                       V.sums[(size_t)7 * P + i] * (cl[1] ? 0.f : 1.f),
+                                       V.sums[(size_t)8 * P + i] * (cl[2] ? 0.f : 1.f)};
+                float basis[16];
+                sh_basis16(x, y, z, basis);
+#pragma unroll
+                for (int k = 0; k < MC; ++k)
+                    if (k < active) {
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) s_row[3 * k + c] += basis[k] * dRGB[c];
+                    }
+            }
         }
         __syncthreads();
         if (a.accm & GSR_GRAD_SH) sh_rows_from_lds<MC, true>(s_sh, nrow, a.dL_dsh + (size_t)i0 * RL);
@@ -1280,6 +1254,12 @@ hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s) {
 template <int MC>
 static void gauss_bwd_multi_mc(const MultiArgs &a, hipStream_t s) {
     k_gauss_bwd_multi<MC><<<div_up(a.P, kShBlock), kShBlock, multi_lds_bytes<MC>(), s>>>(a);
+}
+
+hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s) {
+    if (P == 0) return hipSuccess;
+    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums);
+    return hipGetLastError();
 }
 
 hipError_t launch_gauss_bwd_multi(const MultiArgs &a, hipStream_t s) {

@@ -69,6 +69,9 @@ hipError_t launch_bwd_items_raw(int K, int T, const uint2 *ranges, const uint32_
                                 hipStream_t s, const uint32_t *spec_ok = nullptr);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
+// Each Gaussian's per-pair records of one view summed in emission order into kPartial x P SoA sums
+// (the deferred multi-view pass reads these instead of walking the records itself).
+hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s);
 
 // Per-Gaussian backward over several views of the same Gaussians (gsr_backward_gaussians): one
 // launch reads the parameters and read-modify-writes every gradient once for up to kMultiViews views.
@@ -78,10 +81,9 @@ struct MultiView {
     CamStrides cs;
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const int *radii;
-    const uint32_t *goff;   // the view's emission offsets (GEOM)
     const float4 *rec;      // the view's render records (GEOM): the activated opacity (sigmoid chain)
     const uint8_t *clampm;  // the view's SH clamp masks (GEOM)
-    const float4 *part;     // the view's per-pair records (SCRATCH, gsr_backward_render)
+    const float *sums;      // the view's per-Gaussian record sums, kPartial x P SoA (SUMS, gsr_backward_render)
     float *dL_dmeans2D;     // the view's screen-space gradient (P,3) or NULL
     int acc2;               // add into dL_dmeans2D instead of overwriting
 };

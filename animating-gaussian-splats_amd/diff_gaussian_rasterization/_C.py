@@ -24,7 +24,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIB", os.path.join(_HERE, "libgsr.so"))
 
-GSR_BUF_GEOM, GSR_BUF_BINNING, GSR_BUF_IMAGE, GSR_BUF_SCRATCH = 0, 1, 2, 3
+GSR_BUF_GEOM, GSR_BUF_BINNING, GSR_BUF_IMAGE, GSR_BUF_SCRATCH, GSR_BUF_SUMS = 0, 1, 2, 3, 4
 EXPORTED_SYMBOLS = (
     "gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_geom_bytes", "gsr_image_bytes",
     "gsr_binning_bytes", "gsr_scratch_bytes", "gsr_last_error", "gsr_abi_version",
@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
-    "gsr_forward_info_call", "gsr_spec_stats",
+    "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes",
 )
 
 
@@ -111,6 +111,8 @@ def load_library():
     for n in ("gsr_geom_bytes", "gsr_binning_bytes"):
         getattr(L, n).restype = ctypes.c_size_t
         getattr(L, n).argtypes = [i]
+    L.gsr_sums_bytes.restype = ctypes.c_size_t
+    L.gsr_sums_bytes.argtypes = [i]
     for n in ("gsr_scratch_bytes", "gsr_backward_items_bytes"):
         getattr(L, n).restype = ctypes.c_size_t
         getattr(L, n).argtypes = [i, i, i]
@@ -140,7 +142,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 14  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 15  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -384,8 +386,9 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
                                         binningBuffer, imageBuffer, activations=0, prepare_backward=False,
                                         binning_layout=0):
     """The per-pixel half of ``rasterize_gaussians_backward`` (gsr_backward_render): returns the
-    view's SCRATCH byte buffer holding its per-(tile, Gaussian) gradient records, for
-    ``rasterize_gaussians_backward_views``."""
+    view's SUMS byte buffer (each Gaussian's per-(tile, Gaussian) gradient records summed, 9 x P
+    floats), for ``rasterize_gaussians_backward_views``; the records' SCRATCH buffer is released here
+    (its last reader is already queued on the current stream)."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
@@ -403,7 +406,7 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
         _check(L.gsr_backward_render(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
                                      geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
                                      dpix.data_ptr(), alloc.cb, None, _stream_ptr(dev)))
-    return alloc.buffers[GSR_BUF_SCRATCH]
+    return alloc.buffers[GSR_BUF_SUMS]
 
 
 def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations, scale_modifier,

@@ -43,7 +43,7 @@ PMC_SUMMARY = os.path.join(REPO, "profiles", "r02_hbm_pmc.json")
 SQ_SUMMARY = os.path.join(REPO, "profiles", "r02_sq_pmc.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
 PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "bwd_items",
-          "render_bwd", "gauss_bwd"]
+          "render_bwd", "sum_records", "gauss_bwd"]
 
 
 def streamed_read_bytes(phase, P, K, N, T):

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 14
+#define GSR_ABI_VERSION 15
 
 enum gsr_status {
     GSR_OK = 0,
@@ -47,7 +47,8 @@ enum gsr_status {
  * geometryBuffer / binningBuffer / imageBuffer resize functors (rasterize_points.cu), plus the
  * backward pass's transient scratch.  The caller owns every returned buffer; GEOM, BINNING and
  * IMAGE must be kept alive and handed back to gsr_backward. */
-enum gsr_buffer { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2, GSR_BUF_SCRATCH = 3 };
+enum gsr_buffer { GSR_BUF_GEOM = 0, GSR_BUF_BINNING = 1, GSR_BUF_IMAGE = 2, GSR_BUF_SCRATCH = 3,
+                  GSR_BUF_SUMS = 4 /* ABI >= 15: gsr_backward_render's per-Gaussian record sums */ };
 
 /* Returns a device pointer of at least `bytes` bytes, 256-byte aligned, or NULL on failure. */
 typedef void *(*gsr_alloc_fn)(void *ctx, int which, size_t bytes);
@@ -182,10 +183,13 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
  * gsr_backward split in two so that the per-Gaussian half runs ONCE for all the views of a step
  * (train.py:753-767 sums the losses of 5 views before one backward):
  *
- *   gsr_backward_render     the per-pixel half of gsr_backward for one view: requests its SCRATCH
- *                           buffer through `alloc` and fills it with the view's per-(tile, Gaussian)
- *                           gradient records.  Keep SCRATCH (and the view's GEOM, radii) alive until
- *                           gsr_backward_gaussians has been queued.
+ *   gsr_backward_render     the per-pixel half of gsr_backward for one view: requests a SCRATCH
+ *                           buffer through `alloc` for the view's per-(tile, Gaussian) gradient
+ *                           records, then a SUMS buffer (gsr_sums_bytes(P), ABI >= 15) into which it
+ *                           sums each Gaussian's records in emission order (9 x P floats, SoA).  Only
+ *                           SUMS (and the view's GEOM, radii) must stay alive until
+ *                           gsr_backward_gaussians has been queued; SCRATCH may be released once the
+ *                           call returns (its last reader is queued on `stream`).
  *   gsr_backward_gaussians  the per-Gaussian half over `nviews` such views of the SAME Gaussians `g`:
  *                           every per-Gaussian gradient of `out` receives the SUM over the views
  *                           (added into the arrays marked in out->accumulate, as gsr_backward does);
@@ -200,7 +204,8 @@ typedef struct gsr_view_grad {
     const gsr_camera *cam;   /* the view's camera (as given to its gsr_forward) */
     const int *radii;        /* the view's radii (P) */
     const void *geom;        /* the view's GEOM buffer */
-    const void *scratch;     /* the view's SCRATCH buffer, filled by gsr_backward_render */
+    const void *scratch;     /* the view's SUMS buffer, filled by gsr_backward_render (ABI >= 15;
+                                the SCRATCH buffer before) */
     int num_rendered;        /* the view's num_rendered */
     float *dL_dmeans2D;      /* (P,3) the view's screen-space gradient, or NULL */
     int accumulate_means2D;  /* nonzero: add into dL_dmeans2D instead of overwriting it */
@@ -230,6 +235,7 @@ size_t gsr_geom_bytes(int P);
 size_t gsr_image_bytes(int width, int height, int P);
 size_t gsr_binning_bytes(int num_rendered);
 size_t gsr_scratch_bytes(int num_rendered, int width, int height);
+size_t gsr_sums_bytes(int P);  /* ABI >= 15: the SUMS buffer of gsr_backward_render */
 /* Extra BINNING bytes gsr_forward requests when gsr_gaussians.prepare_backward is set (ABI 12). */
 size_t gsr_backward_items_bytes(int num_rendered, int width, int height);
 
@@ -355,7 +361,7 @@ int gsr_views_pack(int frames, int H, int W, const uint8_t *rgb, const uint8_t *
 
 /* Per-phase device timing with HIP events recorded on the call's stream (off by default).
  * Phases: "preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd",
- * "bwd_items", "render_bwd", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam", "views_pack".  gsr_profile_read synchronises on the recorded events. */
+ * "bwd_items", "render_bwd", "sum_records", "gauss_bwd", "ssim_fwd", "ssim_bwd", "densify_plan", "densify_apply", "adam", "views_pack".  gsr_profile_read synchronises on the recorded events. */
 int gsr_profile_enable(int on);
 /* Restrict event recording to a comma-separated list of phases (NULL or "" = every phase), so a
  * timed region can carry the events of one kernel only.  Host-side timers are unaffected. */

@@ -12,6 +12,6 @@ for rep in ${REPS:-1 2 3}; do
     python -c "
 import json; d=json.loads([l for l in open('gpurun_out/abenv/v$k.$rep.json') if l.startswith('{')][0])
 p=d['phase_ms_per_launch']; s=d['phase_ms_per_launch_solo']
-print('$e rep=$rep', d['value'], d['median_ms_per_step'], d['value_mean'], d['step_ms_quartiles'], {k: (round(s[k]*1e3), round(p[k]*1e3)) for k in ('render_fwd','render_bwd','gauss_bwd','bin_emit','bin_count')})"
+print('$e rep=$rep', d['value'], d['median_ms_per_step'], d['value_mean'], d['step_ms_quartiles'], {k: (round(s[k]*1e3), round(p[k]*1e3)) for k in ('render_fwd','render_bwd','sum_records','gauss_bwd','bin_emit','bin_count') if k in s})"
   done
 done
