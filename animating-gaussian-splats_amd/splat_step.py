@@ -7,7 +7,9 @@ drop-in ``GaussianRasterizer`` for the benchmark and the parity tests alike:
 
 * the views alternate over ``streams`` (one view's memory-bound kernels overlap the next view's
   VALU-bound blend kernels; libgsr orders the gradient writes across streams, so the result is
-  bitwise that of one stream -- ``tests/test_streams.py``);
+  bitwise that of one stream -- ``tests/test_streams.py``); ``rotate``: the assignment starts one
+  stream further every call, so with 5 views on 3 streams the streams carry 2, 2, 1 views in turn
+  instead of the first two always carrying two (their serial kernel chains bound the step);
 * ``threads``: one host thread per stream submits that stream's forwards, so a forward waiting for
   its ``num_rendered`` read-back (the reference's host sync) blocks only its own stream;
 * ``summed``: the views' images are backpropagated together (``torch.autograd.backward`` of all
@@ -22,6 +24,7 @@ reference's call site, train.py:354-364).
 """
 from __future__ import annotations
 
+import os
 from concurrent.futures import ThreadPoolExecutor
 from typing import Callable, Sequence
 
@@ -32,12 +35,14 @@ from diff_gaussian_rasterization import GaussianRasterizer
 
 class RenderStep:
     def __init__(self, device, cams: Sequence, inputs_of: Callable, dl: torch.Tensor, streams: Sequence,
-                 threads: bool = True, shape: str = "summed"):
+                 threads: bool = True, shape: str = "summed", rotate: bool | None = None):
         if shape not in ("summed", "per_view"):
             raise ValueError(f"shape: 'summed' or 'per_view', got {shape!r}")
         self.device, self.cams, self.inputs_of, self.dl = device, cams, inputs_of, dl
         self.streams = list(streams)
         self.shape = shape
+        self.rotate = os.environ.get("GSR_STREAM_ROTATE", "1") != "0" if rotate is None else rotate
+        self.calls = 0
         self.pool = ThreadPoolExecutor(max_workers=len(self.streams)) if threads and len(self.streams) > 1 else None
 
     def close(self):
@@ -63,23 +68,26 @@ class RenderStep:
         the order of ``views``."""
         ns = 1 if solo else len(self.streams)
         pool = None if solo else self.pool
+        off = self.calls % ns if self.rotate else 0  # stream of this call's first view
+        self.calls += 1
+        streams = self.streams[off:ns] + self.streams[:off] if ns > 1 else self.streams[:1]
         if self.shape == "summed":
             if pool is not None:
-                futs = [pool.submit(self._forwards, views[k::ns], self.streams[k]) for k in range(min(ns, len(views)))]
+                futs = [pool.submit(self._forwards, views[k::ns], streams[k]) for k in range(min(ns, len(views)))]
                 imgs = [None] * len(views)
                 for k, f in enumerate(futs):
                     imgs[k::ns] = f.result()
             else:
                 imgs = []
                 for k, ci in enumerate(views):
-                    imgs += self._forwards([ci], self.streams[k % ns])
+                    imgs += self._forwards([ci], streams[k % ns])
             torch.autograd.backward(imgs, [self.dl] * len(imgs))
             return [img.detach() for img in imgs]
         elif pool is not None:
-            futs = [pool.submit(self._fwd_bwd, views[k::ns], self.streams[k]) for k in range(min(ns, len(views)))]
+            futs = [pool.submit(self._fwd_bwd, views[k::ns], streams[k]) for k in range(min(ns, len(views)))]
             for f in futs:
                 f.result()
         else:
             for k, ci in enumerate(views):
-                self._fwd_bwd([ci], self.streams[k % ns])
+                self._fwd_bwd([ci], streams[k % ns])
         return None
