@@ -585,6 +585,10 @@ def main():
                          "for per-view; threads: one host thread per stream submits that stream's views, so a forward "
                          "waiting for its num_rendered read-back blocks only its own thread and the other "
                          "streams' views keep the GPU fed; serial: one thread submits every view in turn")
+    ap.add_argument("--means2d", default="per-view", choices=["per-view", "shared"],
+                    help="per-view (default): every render gets a fresh zero means2D leaf, as "
+                         "create_render_arguments makes one per render (shared.py:38-41); shared: one "
+                         "means2D leaf for all views of a step")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path on one GPU)")
@@ -705,7 +709,12 @@ def main():
 
     if args.submit == "auto":
         args.submit = "threads" if args.step_shape == "summed" else "serial"
-    rstep = splat_step.RenderStep(dev, cams, lambda ci: leaves, dl, streams, threads=args.submit == "threads",
+    def inputs_of(ci):  # called on the view's stream (RenderStep), like the reference's per-render zeros
+        if args.means2d == "shared":
+            return leaves
+        return dict(leaves, means2D=torch.zeros_like(leaves["means3D"], requires_grad=True))
+
+    rstep = splat_step.RenderStep(dev, cams, inputs_of, dl, streams, threads=args.submit == "threads",
                                   shape="summed" if args.step_shape == "summed" else "per_view")
 
     def step(it, solo=False, keep=False):
@@ -975,6 +984,8 @@ def main():
                        "streams_per_gpu": len(streams),
                        "step_shape": "per frame: view losses summed, one backward, one Adam step" if c5_cfg else shape,
                        "submission": "one host thread per stream" if rstep.pool is not None else "one host thread",
+                       "means2D": None if c5_cfg else ("one fresh zero leaf per render (shared.py:38-41)"
+                                                       if args.means2d == "per-view" else "one leaf shared by the step's views"),
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
