@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--steps", default=None,
                     help="A:B -- the window from the end of the A-th to the end of the B-th k_gauss_bwd_multi "
                          "launch (one per step; bench.py's timed region at warmup 5 + probe 3 + solo 3: 10:30)")
+    ap.add_argument("--gaps", type=float, default=0.0,
+                    help="also list each stream's idle gaps longer than this many us by (previous kernel -> "
+                         "next kernel): where the serial chain waits (host submission, cross-stream events)")
     a = ap.parse_args()
     rows = []
     for f in glob.glob(os.path.join(a.trace_dir, "**", "*kernel_trace.csv"), recursive=True):
@@ -60,6 +63,16 @@ def main():
         print(f"stream {sid}: {len(rs)} kernels, busy {busy / span:.3f} of the window, idle gaps {sum(gaps) / 1e3:.0f} us "
               f"(mean {sum(gaps) / max(len(gaps), 1) / 1e3:.1f} us)")
         print("   " + ", ".join(f"{n} {v:.0f}" for n, v in top))
+        if a.gaps > 0:
+            where = defaultdict(list)
+            last, prev = None, None
+            for s, e, _, n in rs:
+                if last is not None and s - last > a.gaps * 1e3:
+                    where[(prev, n)].append((s - last) / 1e3)
+                if last is None or e > last:
+                    last, prev = e, n
+            for (p0, p1), v in sorted(where.items(), key=lambda kv: -sum(kv[1]))[:8]:
+                print(f"     gap {p0} -> {p1}: n={len(v)} total {sum(v):.0f} us mean {sum(v) / len(v):.1f} us")
 
 
 if __name__ == "__main__":
