@@ -256,6 +256,16 @@ size_t gsr_scratch_bytes(int K, int W, int H) {
     return ScratchLayout(K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH)).total;
 }
 
+void *gsr_prealloc_alloc(void *ctx, int which, size_t bytes) {
+    gsr_prealloc *pa = (gsr_prealloc *)ctx;
+    if (!pa) return nullptr;
+    if (which >= 0 && which < 5 && pa->ptr[which] && pa->bytes[which] >= bytes && !(pa->used & (1 << which))) {
+        pa->used |= 1 << which;
+        return pa->ptr[which];
+    }
+    return pa->fallback ? pa->fallback(pa->fallback_ctx, which, bytes) : nullptr;
+}
+
 int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const GeomLayout g(P);
     const ImageLayout im(W, H, P);
@@ -306,6 +316,19 @@ void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
     if (outcome < 0) ++g_spec_misses;
 }
 
+}  // namespace
+
+extern "C" size_t gsr_spec_binning_bytes(int P, int W, int H, int prepare_backward) {
+    if (P <= 0 || W <= 0 || H <= 0) return 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const uint32_t cap = spec_capacity(SpecKey{dev, P, W, H});
+    if (!cap) return 0;
+    const size_t items = (GSR_FWD_ITEMS && prepare_backward) ? bwd_items_bytes((int)cap, div_up(W, kTileW) * div_up(H, kTileH)) : 0;
+    return BinningLayout((int)cap).total + items;
+}
+
+namespace {
 int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
                  float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, bool speculate,
                  void *stream) {

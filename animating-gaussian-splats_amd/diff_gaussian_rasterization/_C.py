@@ -10,14 +10,18 @@ diff-gaussian-rasterization-w-depth submodule, ``/root/reference/.gitmodules:1-3
 * ``mark_visible(means3D, viewmatrix, projmatrix) -> bool[P]``
 
 Tensors cross the boundary as raw device pointers (``include/gsr.h``); the three persistent
-workspaces are ``torch.uint8`` tensors allocated through a ctypes callback so their lifetime follows
-the autograd graph, like the reference's ``resizeFunctional`` byte buffers.  There is no CPU path:
+workspaces are ``torch.uint8`` tensors whose lifetime follows the autograd graph, like the reference's
+``resizeFunctional`` byte buffers.  They are sized and allocated here before the native call and handed
+out by ``gsr_prealloc_alloc`` (C), so a call makes no callback into Python on its usual path; a request
+the pre-sized buffers do not cover (a first or redone speculative forward) falls back to a ctypes
+callback.  There is no CPU path:
 a missing ``libgsr.so`` or a CPU tensor raises.
 """
 from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -33,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "gsr_densify_update_radii", "gsr_densify_accumulate_grads", "gsr_densify_workspace_bytes",
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
-    "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes",
+    "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes", "gsr_prealloc_alloc", "gsr_spec_binning_bytes",
 )
 
 
@@ -73,7 +77,15 @@ class _ViewGrad(ctypes.Structure):  # gsr_view_grad (ABI 12)
 
 
 _ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
+
+
+class _Prealloc(ctypes.Structure):  # gsr_prealloc (ABI 16)
+    _fields_ = [("ptr", ctypes.c_void_p * 5), ("bytes", ctypes.c_size_t * 5), ("fallback", _ALLOC_FN),
+                ("fallback_ctx", ctypes.c_void_p), ("used", ctypes.c_int)]
+
+
 _lib = None
+_PREALLOC_FN = None  # gsr_prealloc_alloc as a gsr_alloc_fn (a C function: no Python on the call path)
 
 
 def load_library():
@@ -136,13 +148,17 @@ def load_library():
     L.gsr_l1_ssim_forward.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp]
     L.gsr_l1_ssim_backward.restype = i
     L.gsr_l1_ssim_backward.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, vp]
+    L.gsr_spec_binning_bytes.restype = ctypes.c_size_t
+    L.gsr_spec_binning_bytes.argtypes = [i, i, i, i]
     if L.gsr_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libgsr.so ABI {L.gsr_abi_version()} != binding ABI {ABI_VERSION}: rebuild it")
+    global _PREALLOC_FN
+    _PREALLOC_FN = _ALLOC_FN(ctypes.cast(L.gsr_prealloc_alloc, ctypes.c_void_p).value)
     _lib = L
     return L
 
 
-ABI_VERSION = 15  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 16  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -168,24 +184,64 @@ def _f32(t):
     return t.contiguous() if t is not None and t.numel() else t
 
 
-class _Allocator:
-    """ctypes allocation callback handing out torch byte tensors on the current device.  The callback
-    closes over the buffer dict only -- a callback bound to the allocator itself would make a reference
-    cycle that keeps every workspace alive until Python's cyclic collector runs (GBs at C3)."""
+_tls = threading.local()
 
-    def __init__(self, device):
+
+def _fallback_alloc(_ctx, which, nbytes):
+    """The pre-allocation's fallback (a request the pre-sized buffers do not cover: a first forward,
+    a redone speculation): a byte tensor on the calling thread's current pre-allocation device."""
+    try:
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=_tls.device)
+    except Exception:  # noqa: BLE001 - reported through the C ABI as GSR_ERR_ALLOC
+        return None
+    _tls.buffers[int(which)] = t
+    return t.data_ptr()
+
+
+_FALLBACK_FN = _ALLOC_FN(_fallback_alloc)  # one thunk for the process
+_PREALLOC_ON = os.environ.get("GSR_PREALLOC", "1") != "0"  # 0: every request through the callback (A/B)
+
+
+class _PreAllocator:
+    """Buffers sized on the host before the native call and handed out by gsr_prealloc_alloc (C),
+    so the call makes no ctypes callback (which would re-acquire the interpreter lock while other
+    threads submit their views) unless a request exceeds them.  ``sizes``: {gsr_buffer: bytes};
+    buffers given as one list are carved from ONE allocation (they share its lifetime)."""
+
+    def __init__(self, device, groups):
         self.device = device
-        buffers = self.buffers = {}
+        self.pa = _Prealloc()
+        self.given = {}
+        for group in groups if _PREALLOC_ON else ():
+            offs, total = [], 0
+            for which, nbytes in group:
+                offs.append((which, total, nbytes))
+                total += (int(nbytes) + 255) & ~255
+            if total == 0:
+                continue
+            buf = torch.empty(total, dtype=torch.uint8, device=device)
+            for which, o, nbytes in offs:
+                if nbytes > 0:
+                    t = buf.narrow(0, o, int(nbytes))
+                    self.given[which] = t
+                    self.pa.ptr[which] = t.data_ptr()
+                    self.pa.bytes[which] = int(nbytes)
+        self.pa.fallback = _FALLBACK_FN
+        self.cb = _PREALLOC_FN
+        self.ctx = ctypes.byref(self.pa)
 
-        def alloc(_ctx, which, nbytes):
-            try:
-                t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
-            except Exception:  # noqa: BLE001 - reported through the C ABI as GSR_ERR_ALLOC
-                return None
-            buffers[int(which)] = t
-            return t.data_ptr()
+    def __enter__(self):
+        self.prev = getattr(_tls, "buffers", None), getattr(_tls, "device", None)
+        _tls.buffers, _tls.device = {}, self.device
+        return self
 
-        self.cb = _ALLOC_FN(alloc)
+    def __exit__(self, *exc):
+        got = _tls.buffers
+        _tls.buffers, _tls.device = self.prev
+        # what the call took: the pre-allocated tensors it was handed, and the fallback's
+        self.buffers = {w: t for w, t in self.given.items() if (self.pa.used >> w) & 1}
+        self.buffers.update(got)
+        return False
 
 
 class _device_guard:
@@ -282,12 +338,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
     depth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
     radii = torch.empty((P,), dtype=torch.int32, device=dev)  # preprocess writes every entry
-    alloc = _Allocator(dev)
     fi = _ForwardInfo(0, 0, 0)
     with _device_guard(dev):  # launches go to dev even when another device is current
-        _check(L.gsr_forward_info_call(ctypes.byref(cam), ctypes.byref(g), alloc.cb, None, color.data_ptr(),
-                                       depth.data_ptr(), radii.data_ptr() if P else None, int(bool(speculate)),
-                                       ctypes.byref(fi), _stream_ptr(dev)))
+        # GEOM, IMAGE and (when this forward will speculate) BINNING sized here, in one allocation
+        spec = L.gsr_spec_binning_bytes(P, W, H, int(bool(prepare_backward))) if speculate and P else 0
+        alloc = _PreAllocator(dev, [[(GSR_BUF_GEOM, L.gsr_geom_bytes(P)), (GSR_BUF_IMAGE, L.gsr_image_bytes(W, H, P)),
+                                     (GSR_BUF_BINNING, spec)]])
+        with alloc:
+            _check(L.gsr_forward_info_call(ctypes.byref(cam), ctypes.byref(g), alloc.cb, alloc.ctx, color.data_ptr(),
+                                           depth.data_ptr(), radii.data_ptr() if P else None, int(bool(speculate)),
+                                           ctypes.byref(fi), _stream_ptr(dev)))
     if info is not None:
         info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated))
     b = alloc.buffers
@@ -372,11 +432,11 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     dpix = dL_dout_color.contiguous().float()
     keep.append(dpix)
     grads = _Grads(*[t.data_ptr() if t is not None and t.numel() else None for t in out], acc_bits)
-    alloc = _Allocator(dev)
-    with _device_guard(dev):
+    alloc = _PreAllocator(dev, [[(GSR_BUF_SCRATCH, L.gsr_scratch_bytes(int(R), W, H))]])
+    with _device_guard(dev), alloc:
         _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
                               geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
-                              dpix.data_ptr(), None, alloc.cb, None, ctypes.byref(grads), _stream_ptr(dev)))
+                              dpix.data_ptr(), None, alloc.cb, alloc.ctx, ctypes.byref(grads), _stream_ptr(dev)))
     return out
 
 
@@ -401,11 +461,13 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
         return torch.empty(1, dtype=torch.uint8, device=dev)
     dpix = dL_dout_color.contiguous().float()
     keep.append(dpix)
-    alloc = _Allocator(dev)
-    with _device_guard(dev):
+    # SCRATCH and SUMS as two allocations: SCRATCH is released when this returns, SUMS stays queued
+    alloc = _PreAllocator(dev, [[(GSR_BUF_SCRATCH, L.gsr_scratch_bytes(int(R), W, H))],
+                                [(GSR_BUF_SUMS, L.gsr_sums_bytes(P))]])
+    with _device_guard(dev), alloc:
         _check(L.gsr_backward_render(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
                                      geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
-                                     dpix.data_ptr(), alloc.cb, None, _stream_ptr(dev)))
+                                     dpix.data_ptr(), alloc.cb, alloc.ctx, _stream_ptr(dev)))
     return alloc.buffers[GSR_BUF_SUMS]
 
 

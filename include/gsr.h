@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 15
+#define GSR_ABI_VERSION 16
 
 enum gsr_status {
     GSR_OK = 0,
@@ -238,6 +238,28 @@ size_t gsr_scratch_bytes(int num_rendered, int width, int height);
 size_t gsr_sums_bytes(int P);  /* ABI >= 15: the SUMS buffer of gsr_backward_render */
 /* Extra BINNING bytes gsr_forward requests when gsr_gaussians.prepare_backward is set (ABI 12). */
 size_t gsr_backward_items_bytes(int num_rendered, int width, int height);
+
+/* Pre-allocated buffers (ABI >= 16).  gsr_prealloc_alloc is a gsr_alloc_fn (ctx = a gsr_prealloc)
+ * that hands out ptr[which] when bytes[which] covers the request and passes every other request to
+ * `fallback` (NULL: the request fails).  A caller that sizes the buffers beforehand (the functions
+ * above and gsr_spec_binning_bytes) gets no call back into its own allocator on the usual path --
+ * a Python caller's allocator needs the interpreter lock, which a forward otherwise re-acquires three
+ * times while other threads submit their views.  `used` (output): bit k set when ptr[k] was handed
+ * out. */
+typedef struct gsr_prealloc {
+    void *ptr[5];          /* indexed by gsr_buffer */
+    size_t bytes[5];
+    gsr_alloc_fn fallback;
+    void *fallback_ctx;
+    int used;
+} gsr_prealloc;
+void *gsr_prealloc_alloc(void *ctx, int which, size_t bytes);
+/* The BINNING bytes a speculative gsr_forward_info_call with these sizes on the current device will
+ * request (the capacity from its pair-count history, plus the backward's item list when
+ * prepare_backward is set), or 0 when it will not speculate (no history, or the last forward of
+ * these sizes needed the long-list merge sort).  Another thread's forward may raise the capacity
+ * meanwhile: a larger request then goes to the fallback. */
+size_t gsr_spec_binning_bytes(int P, int width, int height, int prepare_backward);
 
 /* Introspection for parity tests: byte offsets of the arrays inside the three forward buffers, in
  * this order: geom {depth, rec (64-byte render records), rect, tiles, goff}, image {ranges,
