@@ -581,14 +581,17 @@ def main():
                          "views at the end of the pass (deferred multi-view backward); per-view: a "
                          "backward per view")
     ap.add_argument("--submit", default="auto", choices=["auto", "threads", "serial"],
-                    help="auto: threads for the summed step (+4 %% measured: tools/ab_submit.sh), serial "
-                         "for per-view; threads: one host thread per stream submits that stream's views, so a forward "
+                    help="auto: threads for the summed step (C3: +3-5 %% measured, tools/ab_args.sh), serial "
+                         "for per-view and C2 (small views: one thread is faster and steadier); threads: one host thread per stream submits that stream's views, so a forward "
                          "waiting for its num_rendered read-back blocks only its own thread and the other "
                          "streams' views keep the GPU fed; serial: one thread submits every view in turn")
     ap.add_argument("--means2d", default="per-view", choices=["per-view", "shared"],
                     help="per-view (default): every render gets a fresh zero means2D leaf, as "
                          "create_render_arguments makes one per render (shared.py:38-41); shared: one "
                          "means2D leaf for all views of a step")
+    ap.add_argument("--gil-switch-us", type=float, default=0.0,
+                    help="sys.setswitchinterval in microseconds for the submitting threads (0: Python's "
+                         "default, 5000)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse the multi-rank path on one GPU)")
@@ -624,6 +627,8 @@ def main():
     if args.views_per_rank is None:
         args.views_per_rank = 4 if args.config == "C2" else 5
 
+    if args.gil_switch_us > 0:
+        sys.setswitchinterval(args.gil_switch_us * 1e-6)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_self_launch(args.gpus))
 
@@ -708,7 +713,11 @@ def main():
         _C.grad_fence(*grads_of())
 
     if args.submit == "auto":
-        args.submit = "threads" if args.step_shape == "summed" else "serial"
+        # threads: one submitting thread per stream pays off when a view's GPU work (~0.7 ms at C3)
+        # covers the thread hand-offs; C2's views (~0.3 ms) run faster and steadier from one thread
+        # (C2 threads 200-418 vs serial 265-277 Msplats/s; C3 threads +3-5 %, tools/ab_args.sh)
+        args.submit = "threads" if args.step_shape == "summed" and args.config != "C2" else "serial"
+
     def inputs_of(ci):  # called on the view's stream (RenderStep), like the reference's per-render zeros
         if args.means2d == "shared":
             return leaves
