@@ -231,7 +231,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.meta = (uint32_t *)(base + L.meta); a.chunk_off = (uint32_t *)(base + L.chunk_off);
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
-    const BinningLayout L(K);
+    const BinningLayout L(K, a.P);
     a.pairs = (uint4 *)(base + L.pairs);
     a.point_list = (uint32_t *)(base + L.point_list);
     a.slot_emit = (uint32_t *)(base + L.slot_emit);
@@ -247,7 +247,7 @@ int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
 size_t gsr_geom_bytes(int P) { return GeomLayout(P < 0 ? 0 : P).total; }
 size_t gsr_image_bytes(int W, int H, int P) { return ImageLayout(W, H, P < 0 ? 0 : P).total; }
-size_t gsr_binning_bytes(int K) { return BinningLayout(K).total; }
+size_t gsr_binning_bytes(int K, int P) { return BinningLayout(K, P).total; }
 size_t gsr_backward_items_bytes(int K, int W, int H) {
     return bwd_items_bytes(K < 0 ? 0 : K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH));
 }
@@ -269,7 +269,7 @@ void *gsr_prealloc_alloc(void *ctx, int which, size_t bytes) {
 int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const GeomLayout g(P);
     const ImageLayout im(W, H, P);
-    const BinningLayout b(K);
+    const BinningLayout b(K, P);
     const size_t v[14] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
                           im.ranges, im.pix_end, im.n_contrib, im.tile_maxc,
                           b.pairs, b.point_list, b.slot_emit, im.seg_off, b.seg_state};
@@ -325,7 +325,7 @@ extern "C" size_t gsr_spec_binning_bytes(int P, int W, int H, int prepare_backwa
     const uint32_t cap = spec_capacity(SpecKey{dev, P, W, H});
     if (!cap) return 0;
     const size_t items = (GSR_FWD_ITEMS && prepare_backward) ? bwd_items_bytes((int)cap, div_up(W, kTileW) * div_up(H, kTileH)) : 0;
-    return BinningLayout((int)cap).total + items;
+    return BinningLayout((int)cap, P).total + items;
 }
 
 namespace {
@@ -354,7 +354,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     if (a.P == 0) {  // reference: colour/depth stay zero (no background) when there are no Gaussians
         HIP_TRY(launch_zero(out_color, 3 * npix, s));
         HIP_TRY(launch_zero(out_depth, npix, s));
-        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout(0).total);
+        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout(0, 0).total);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning)");
         return GSR_OK;
     }
@@ -372,7 +372,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, hw.d, s)); }
     const size_t spec_item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;
     if (cap) {  // speculative: the post-scan kernels are queued now, against the capacity
-        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)cap).total + spec_item_bytes);
+        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)cap, a.P).total + spec_item_bytes);
         if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, capacity %u)", cap);
         carve_binning(a, bin, (int)cap);
         a.spec_ok = a.meta + 1;
@@ -381,8 +381,8 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
         if (GSR_FWD_ITEMS && g->prepare_backward) {
             Phase ph(s, "bwd_items");
-            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.ranges, a.tile_maxc,
-                                         (uint2 *)(bin + BinningLayout((int)cap).total), s, a.spec_ok));
+            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc,
+                                         (uint2 *)(bin + BinningLayout((int)cap, a.P).total), s, a.spec_ok));
         }
     }
     uint32_t K;
@@ -421,7 +421,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     // exact path (also the redo of a failed speculation: its queued kernels returned at once)
     a.spec_ok = nullptr;
     // BINNING = the binning arrays, [the backward's item list], [the long-list merge buffer]
-    const size_t bin_bytes = BinningLayout((int)K).total;
+    const size_t bin_bytes = BinningLayout((int)K, a.P).total;
     const size_t item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)K, T) : 0;
     const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
     char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, bin_bytes + item_bytes + tmp_bytes);
@@ -432,7 +432,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // the backward's item list, built here, off its critical path
         Phase ph(s, "bwd_items");
-        HIP_TRY(launch_bwd_items_raw((int)K, T, a.ranges, a.tile_maxc, (uint2 *)(bin + bin_bytes), s));
+        HIP_TRY(launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, (uint2 *)(bin + bin_bytes), s));
     }
     info->binning_layout = (int)K;
     spec_record(key, K, n_vlong > 0, cap ? -1 : 0);
@@ -508,7 +508,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.part = (float4 *)(scr + SL.part);
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // built by the forward, after the binning arrays
-        a.items = (uint2 *)((char *)binning + BinningLayout(layout).total);
+        a.items = (uint2 *)((char *)binning + BinningLayout(layout, a.P).total);
     } else {
         a.items = (uint2 *)(scr + SL.items);
         Phase ph(s, "bwd_items");

@@ -29,14 +29,15 @@ __device__ uint64_t *g_trace_bwd;
 constexpr uint32_t kItemStartCost = 64;  // init loads + first gathers, in (pair, quarter) steps
 __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restrict__ ranges,
                                                     const uint32_t *__restrict__ tile_maxc,
-                                                    uint2 *__restrict__ items, const uint32_t *__restrict__ spec_ok) {
+                                                    uint2 *__restrict__ items, const uint32_t *__restrict__ spec_ok,
+                                                    int ks) {
     __shared__ uint32_t s_hist[kOrderBuckets];
     __shared__ uint32_t s_red[16];
     if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
     for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
-    constexpr uint32_t kMaxCost = 4u * kSeg + kItemStartCost;
-    constexpr uint32_t kShift = kMaxCost >= (uint32_t)kOrderBuckets ? 32 - __builtin_clz(kMaxCost / kOrderBuckets) : 0;
-    auto bucket = [](uint32_t cost) { return (uint32_t)kOrderBuckets - 1u - min(cost >> kShift, (uint32_t)kOrderBuckets - 1u); };
+    const uint32_t kMaxCost = (4u << ks) + kItemStartCost;
+    const uint32_t kShift = kMaxCost >= (uint32_t)kOrderBuckets ? 32 - __builtin_clz(kMaxCost / kOrderBuckets) : 0;
+    auto bucket = [kShift](uint32_t cost) { return (uint32_t)kOrderBuckets - 1u - min(cost >> kShift, (uint32_t)kOrderBuckets - 1u); };
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
         for (int t0 = 0; t0 < T; t0 += kScanRegs * (int)blockDim.x) {  // kScanRegs tiles' loads in flight
@@ -52,9 +53,9 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 #pragma unroll
             for (int i = 0; i < kScanRegs; ++i) {
                 const uint32_t t = (uint32_t)(t0 + i * (int)blockDim.x + (int)threadIdx.x);
-                const uint32_t J = bwd_item_count(nn[i], mq[i]), Z = bwd_zero_items(nn[i], mq[i]);
+                const uint32_t J = bwd_item_count(nn[i], mq[i], ks), Z = bwd_zero_items(nn[i], mq[i]);
                 for (uint32_t j = 0; j < J + Z; ++j) {
-                    const uint32_t cost = j < J ? bwd_item_cost(j, mq[i]) + kItemStartCost : kItemStartCost;
+                    const uint32_t cost = j < J ? bwd_item_cost(j, mq[i], ks) + kItemStartCost : kItemStartCost;
                     const uint32_t b = bucket(cost);
                     if (pass == 0) atomicAdd(&s_hist[b], 1u);
                     else items[1 + atomicAdd(&s_hist[b], 1u)] = make_uint2(t, j < J ? j : kZeroItem | (j - J));
@@ -142,7 +143,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
-    float4 *__restrict__ part) {
+    float4 *__restrict__ part, int ks) {
     // Each wave of the workgroup takes its own item and its own LDS slice; the waves never
     // synchronise with each other.  Items are in descending cost order, so the kBwdWaves items of
     // one workgroup cost about the same: grouping them keeps the launch's workgroups coarse, which
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
         }
         return;
     }
-    const int s0 = (int)seg * kSeg, s1f = s0 + kSeg;
+    const int s0 = (int)seg << ks, s1f = s0 + (1 << ks);
     const int s1 = min(s1f, maxc);
     if (s1f >= maxc) {  // the tile's last segment item: the first kZeroChunk slots nobody reached
         for (int p = maxc + lane; p < min(n, maxc + (int)kZeroChunk); p += 64) {
@@ -1208,14 +1209,14 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 
 
 // ==========================================================================================
-hipError_t launch_bwd_items_raw(int K, int T, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
+hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
                                 hipStream_t s, const uint32_t *spec_ok) {
     if (K == 0) return hipSuccess;
-    k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items, spec_ok);
+    k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items, spec_ok, seg_log2(P));
     return hipGetLastError();
 }
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
-    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.ranges, a.tile_maxc, a.items, s);
+    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.P, a.ranges, a.tile_maxc, a.items, s);
 }
 
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
@@ -1224,7 +1225,7 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     // item exit at once
     k_render_bwd<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
                                              a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
-                                             a.slot_emit, a.dL_dcolor, a.part);
+                                             a.slot_emit, a.dL_dcolor, a.part, seg_log2(a.P));
     return hipGetLastError();
 }
 

@@ -86,19 +86,30 @@ struct BinGrid {
 #ifndef GSR_KSEG
 #define GSR_KSEG 256
 #endif
-constexpr int kSeg = GSR_KSEG;
+constexpr int kSeg = GSR_KSEG;  // the longest segment
 static_assert(kSeg >= 64 && (kSeg & (kSeg - 1)) == 0, "kSeg: a power of two, >= the forward's 64-entry batch");
-__host__ __device__ inline uint32_t seg_bounds(uint32_t n) { return n > 0 ? (n - 1) / kSeg : 0; }
+constexpr int kSegLog2Max = __builtin_ctz(kSeg), kSegLog2Min = 6;
+// The segment length of a cloud of P Gaussians, log2 (fixed before the pair count is known: the
+// forward's tile scan lays out the boundary states with it).  Small clouds have short lists and few
+// items per launch: the longest item then sets the backward's time (C2, 100k Gaussians at 800x800:
+// render_bwd 114 us at 256-entry segments, 75 us at 64), so the segment shrinks until ~4 P >> ks
+// (about the pair count) gives >= 8192 items; 1M-Gaussian clouds keep kSeg.
+__host__ __device__ inline int seg_log2(int P) {
+    int ks = kSegLog2Max;
+    while (ks > kSegLog2Min && ((4 * (size_t)(P > 0 ? P : 0)) >> ks) < 8192) --ks;
+    return ks;
+}
+__host__ __device__ inline uint32_t seg_bounds(uint32_t n, int ks) { return n > 0 ? (n - 1) >> ks : 0; }
 
 // The backward's work items of a tile with n list entries and per-quarter max n_contrib mq: one per
-// kSeg entries below the largest quarter maximum (at least one per non-empty tile, which also
-// writes the zero records of the entries nobody reached); cost = its (pair, quarter) steps.
-__host__ __device__ inline uint32_t bwd_item_count(uint32_t n, uint4 mq) {
+// segment (2^ks entries) below the largest quarter maximum (at least one per non-empty tile, which
+// also writes the zero records of the entries nobody reached); cost = its (pair, quarter) steps.
+__host__ __device__ inline uint32_t bwd_item_count(uint32_t n, uint4 mq, int ks) {
     const uint32_t maxc = min(max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
-    return n == 0 ? 0u : max(1u, (maxc + kSeg - 1) / kSeg);
+    return n == 0 ? 0u : max(1u, (maxc + (1u << ks) - 1) >> ks);
 }
-__host__ __device__ inline uint32_t bwd_item_cost(uint32_t j, uint4 mq) {
-    const uint32_t s0 = j * kSeg, s1 = s0 + kSeg;
+__host__ __device__ inline uint32_t bwd_item_cost(uint32_t j, uint4 mq, int ks) {
+    const uint32_t s0 = j << ks, s1 = s0 + (1u << ks);
     const uint32_t a = mq.x > s0 ? min(mq.x, s1) - s0 : 0u, b = mq.y > s0 ? min(mq.y, s1) - s0 : 0u;
     const uint32_t c = mq.z > s0 ? min(mq.z, s1) - s0 : 0u, d = mq.w > s0 ? min(mq.w, s1) - s0 : 0u;
     return a + b + c + d;
@@ -113,10 +124,10 @@ __host__ __device__ inline uint32_t bwd_zero_items(uint32_t n, uint4 mq) {
     const uint32_t maxc = min(max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
     return n - maxc > kZeroChunk ? (n - maxc - 1) / kZeroChunk : 0u;
 }
-// the upper bound of the item count the backward launch covers
+// the upper bound of the item count the backward launch covers (for any segment length)
 __host__ __device__ inline size_t max_bwd_items(int K, int T) {
     const size_t k = (size_t)(K > 0 ? K : 0);
-    return k / kSeg + k / kZeroChunk + (k < (size_t)T ? k : (size_t)T) + 1;
+    return (k >> kSegLog2Min) + k / kZeroChunk + (k < (size_t)T ? k : (size_t)T) + 1;
 }
 
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
@@ -151,11 +162,11 @@ struct ImageLayout {
 
 // BINNING (per Gaussian-tile pair, K): sort keys + their emission index, sorted Gaussian list,
 // emission index of every sorted slot (where the backward stores the slot's gradient record), the
-// saved blend state at every interior segment boundary (<= K / kSeg boundaries in total; each 256
-// float4 (C0, C1, C2, T), one per pixel of the tile in row-major order).
+// saved blend state at every interior segment boundary (<= K >> seg_log2(P) boundaries in total;
+// each 256 float4 (C0, C1, C2, T), one per pixel of the tile in row-major order).
 struct BinningLayout {
     size_t pairs, point_list, slot_emit, seg_state, total;
-    __host__ __device__ BinningLayout(int K) {
+    __host__ __device__ BinningLayout(int K, int P) {
         size_t o = 0;
         // one 16-byte record per pair: (index, depth bits, emission index, 0) -- the 64-bit sort key
         // (depth_bits << 32 | index) in .x/.y and its payload in .z, so k_bin_emit's scatter is ONE
@@ -163,14 +174,14 @@ struct BinningLayout {
         pairs = o;      o = align256(o + sizeof(uint4) * (K > 0 ? K : 1));
         point_list = o; o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));
         slot_emit = o;  o = align256(o + sizeof(uint32_t) * (K > 0 ? K : 1));  // sorted slot -> emission
-        seg_state = o;  o = align256(o + sizeof(float4) * kTilePix * (size_t)(K / kSeg + 1));
+        seg_state = o;  o = align256(o + sizeof(float4) * kTilePix * (size_t)(((size_t)(K > 0 ? K : 0) >> seg_log2(P)) + 1));
         total = o;
     }
 };
 
 // The backward's work-item list ([0].x = count, then (tile, segment) in dispatch order): in SCRATCH,
 // or -- when the forward prepares the backward (gsr_gaussians.prepare_backward) -- right after the
-// BINNING arrays (at BinningLayout(K).total), built by the forward.
+// BINNING arrays (at BinningLayout(K, P).total), built by the forward.
 __host__ __device__ inline size_t bwd_items_bytes(int K, int T) { return align256(sizeof(uint2) * (max_bwd_items(K, T) + 1)); }
 
 // SCRATCH (backward): one packed 36-byte partial-gradient record per Gaussian-tile pair, stored at
@@ -547,6 +558,17 @@ __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
     return e;
 }
 __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }
+
+// A workgroup barrier after this wave's LDS stores / no-return LDS atomics, with an explicit
+// s_waitcnt lgkmcnt(0) in front.  __syncthreads()'s release fence normally brings that wait, but the
+// compiler dropped it in one build at k_render_fwd's blend-loop head (its loop-carried s_live mask,
+// lowered by a no-return ds_and, was then read stale by other waves after the barrier: waves of one
+// block left the loop at different batches, the tile's quarter maxima were corrupted and the backward
+// went nondeterministic).  An explicit wait is kept by the compiler.
+__device__ inline void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt / expcnt at maximum, lgkmcnt(0)
+    __syncthreads();
+}
 
 // Make this wave's LDS writes visible to its own later LDS reads (waves of a render block work
 // on different tiles and never synchronise with each other).

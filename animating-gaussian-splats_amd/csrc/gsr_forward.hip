@@ -231,7 +231,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
                                                    uint32_t *host_words,
                                                    uint32_t *__restrict__ tile_order,
                                                    uint32_t *__restrict__ sort_lists,
-                                                   uint32_t *__restrict__ seg_off, uint32_t cap) {
+                                                   uint32_t *__restrict__ seg_off, uint32_t cap, int ks) {
     __shared__ uint32_t s_red[16];
     __shared__ uint32_t s_hist[kOrderBuckets];
     __shared__ uint32_t s_cls[3];
@@ -266,14 +266,14 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
         // backward segment boundaries: exclusive prefix over tiles (index of each tile's first state)
         uint32_t nbs = 0;
 #pragma unroll
-        for (int i = 0; i < kScanRegs; ++i) nbs += (i < c && t0 + i < T) ? seg_bounds(cnt[i]) : 0u;
+        for (int i = 0; i < kScanRegs; ++i) nbs += (i < c && t0 + i < T) ? seg_bounds(cnt[i], ks) : 0u;
         uint32_t nbt;
         uint32_t sex = block_excl_scan_u32(nbs, s_red, &nbt);
 #pragma unroll
         for (int i = 0; i < kScanRegs; ++i) {
             if (i < c && t0 + i < T) {
                 seg_off[t0 + i] = sex;
-                sex += seg_bounds(cnt[i]);
+                sex += seg_bounds(cnt[i], ks);
             }
         }
         if (threadIdx.x == 0) seg_off[T] = nbt;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
     uint32_t carry3 = 0;
     for (int base = 0; base < T; base += blockDim.x) {
         const int t = base + threadIdx.x;
-        const uint32_t nb = t < T ? seg_bounds(tile_count[t]) : 0;
+        const uint32_t nb = t < T ? seg_bounds(tile_count[t], ks) : 0;
         uint32_t tot;
         const uint32_t ex = block_excl_scan_u32(nb, s_red, &tot) + carry3;
         if (t < T) seg_off[t] = ex;
@@ -686,7 +686,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
     float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
-    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok) {
+    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok,
+    int ks) {
     __shared__ uint64_t s_key[kFwdSortCap];
     __shared__ union {
         uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
@@ -769,16 +770,16 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     GSR_FWD_FETCH(0);
 #endif
     for (int base = 0; base < n; base += 64) {
-        __syncthreads();  // previous batch fully consumed; s_live up to date
+        lds_barrier();  // previous batch fully consumed; s_live up to date
         const uint32_t live = s_live;
         if (!live) break;
-        // segment boundary (kSeg entries): this quarter's blend state before entry `base`, the state a
+        // segment boundary (every 2^ks entries): this quarter's blend state before entry `base`, the state a
         // backward segment's reverse walk starts from; stored while the quarter is live, i.e. for
         // every boundary below its pixels' last contributor (done pixels store their final state)
         // (8x8 quarters: every quarter stores while any is live -- the backward reads whole 16x4 strips,
         // which span two quarters; a finished pixel's state is its final one)
-        if (base > 0 && (base & (kSeg - 1)) == 0 && (GSR_FWD_Q8 || ((live >> wv) & 1u))) {
-            const size_t b = (size_t)seg_off[tile] + (uint32_t)base / kSeg - 1u;
+        if (base > 0 && (base & ((1 << ks) - 1)) == 0 && (GSR_FWD_Q8 || ((live >> wv) & 1u))) {
+            const size_t b = (size_t)seg_off[tile] + ((uint32_t)base >> ks) - 1u;
             seg_state[b * kTilePix + bslot] = make_float4(C0, C1, C2, Tt);
         }
         // ---- stage the batch (block-wide) ----
@@ -926,7 +927,7 @@ hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s
     const BinGrid bg(a.P);
     k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
                                   a.block_sums, a.block_off, a.meta, host_words, a.tile_order_f,
-                                  a.sort_lists, a.seg_off, a.spec_cap);
+                                  a.sort_lists, a.seg_off, a.spec_cap, seg_log2(a.P));
     return hipGetLastError();
 }
 
@@ -974,7 +975,7 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                                    a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
-                                   a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok);
+                                   a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P));
     return hipGetLastError();
 }
 

@@ -65,7 +65,7 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
                                hipStream_t s);
 
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s);
-hipError_t launch_bwd_items_raw(int K, int T, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
+hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
                                 hipStream_t s, const uint32_t *spec_ok = nullptr);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);

@@ -120,9 +120,10 @@ def load_library():
     L.gsr_grad_fence.argtypes = [ctypes.POINTER(vp), i, vp]
     L.gsr_mark_visible.restype = i
     L.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
-    for n in ("gsr_geom_bytes", "gsr_binning_bytes"):
-        getattr(L, n).restype = ctypes.c_size_t
-        getattr(L, n).argtypes = [i]
+    L.gsr_geom_bytes.restype = ctypes.c_size_t
+    L.gsr_geom_bytes.argtypes = [i]
+    L.gsr_binning_bytes.restype = ctypes.c_size_t
+    L.gsr_binning_bytes.argtypes = [i, i]
     L.gsr_sums_bytes.restype = ctypes.c_size_t
     L.gsr_sums_bytes.argtypes = [i]
     for n in ("gsr_scratch_bytes", "gsr_backward_items_bytes"):

@@ -233,7 +233,7 @@ int gsr_mark_visible(int P, const float *means3D, const float *viewmatrix, const
 /* Byte sizes of the buffers gsr_forward requests (for callers that pre-allocate pools). */
 size_t gsr_geom_bytes(int P);
 size_t gsr_image_bytes(int width, int height, int P);
-size_t gsr_binning_bytes(int num_rendered);
+size_t gsr_binning_bytes(int num_rendered, int P);  /* ABI >= 16: the boundary states depend on P */
 size_t gsr_scratch_bytes(int num_rendered, int width, int height);
 size_t gsr_sums_bytes(int P);  /* ABI >= 15: the SUMS buffer of gsr_backward_render */
 /* Extra BINNING bytes gsr_forward requests when gsr_gaussians.prepare_backward is set (ABI 12). */
