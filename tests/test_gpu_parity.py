@@ -242,6 +242,30 @@ def test_long_tile_lists(P, cuda):
     check_backward(_gpu_backward(a, rs, cuda, fw, dl), O.backward(st, dl.numpy()), P, 0)
 
 
+@pytest.mark.parametrize("P,ks", [(150_000, 6), (300_000, 7), (600_000, 8)])
+def test_segment_lengths(P, ks, cuda):
+    """The backward's segment length follows the cloud size (seg_log2, gsr_common.h: 64 entries below
+    262144 Gaussians, 128 below 524288, 256 above).  Faint clustered Gaussians (opacity 0.015, a
+    few pixels wide) keep the ~32 centre pixels blending for thousands of list entries (oracle: up to
+    ~18k), so their reverse walks cross many segment boundaries and restart from the blend states the
+    forward saved there."""
+    g = torch.Generator().manual_seed(6)
+    m = torch.zeros(P, 3)
+    m[:, 0] = torch.rand(P, generator=g) * 0.12 - 0.06
+    m[:, 1] = torch.rand(P, generator=g) * 0.12 - 0.06
+    m[:, 2] = torch.rand(P, generator=g) * 2 - 1
+    a = {"means3D": m, "colors_precomp": torch.rand(P, 3, generator=g),
+         "opacities": torch.full((P, 1), 0.015), "scales": torch.full((P, 3), 0.03),
+         "rotations": torch.tensor([[1.0, 0, 0, 0]]).repeat(P, 1)}
+    rs = S.render_settings(64, 64, S.intrinsics(64.0, 64, 64), S.look_at(0, 0, 4), device="cpu")
+    st = _ora_forward(a, rs)
+    assert int(st["n_contrib"].max()) > (4 << ks)  # the walks span more than 4 segments
+    fw = _gpu_forward(a, rs, cuda)
+    check_forward(fw, st)
+    dl = S.upstream_grad(64, 64, device="cpu")
+    check_backward(_gpu_backward(a, rs, cuda, fw, dl), O.backward(st, dl.numpy()), P, 0)
+
+
 def test_wide_frame_global_binning(cuda):
     """A frame of more than kMaxLdsTiles = 16384 tiles (4224 x 1040: 264 x 65 = 17160 tiles) takes
     the binning path that counts and reserves with global atomics instead of the LDS histogram +
