@@ -413,12 +413,25 @@ __device__ inline float3 cov2d(float3 mean, float fx, float fy, float tfx, float
 // Element strides of the camera inputs (gsr_camera, ABI 8): matrix element k (column-major m[k] of
 // the kernels) sits at (k / 4) * m0 + (k % 4) * m1; campos component c at c * c0.
 struct CamStrides { int v0, v1, p0, p1, c0; };
+// The camera inputs are read through the constant address space: their addresses are wave-uniform
+// and no kernel writes them, so these become scalar loads into SGPRs (as plain global pointers next to
+// the kernels' unrestricted output pointers, they were 35 per-lane vector loads into VGPRs per view).
+#ifndef GSR_CAM_SLOAD
+#define GSR_CAM_SLOAD 1
+#endif
+#if GSR_CAM_SLOAD
+typedef const __attribute__((address_space(4))) float *cam_ptr;
+#else
+typedef const float *cam_ptr;
+#endif
 __device__ inline void load_mat16(const float *__restrict__ m, int s0, int s1, float (&out)[16]) {
+    const cam_ptr c = (cam_ptr)m;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) out[k] = m[(k >> 2) * s0 + (k & 3) * s1];
+    for (int k = 0; k < 16; ++k) out[k] = c[(k >> 2) * s0 + (k & 3) * s1];
 }
 __device__ inline float3 load_campos(const float *__restrict__ c, int s) {
-    return c ? make_float3(c[0], c[s], c[2 * s]) : make_float3(0.f, 0.f, 0.f);
+    const cam_ptr p = (cam_ptr)c;
+    return c ? make_float3(p[0], p[s], p[2 * s]) : make_float3(0.f, 0.f, 0.f);
 }
 
 // SH -> RGB for one channel set; `sh` points at the Gaussian's (M,3) coefficients (global or LDS).
