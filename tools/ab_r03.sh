@@ -17,6 +17,6 @@ for rep in ${REPS:-1 2 3}; do
     python -c "
 import json; d=json.loads([l for l in open('gpurun_out/abr3/$v.$rep.json') if l.startswith('{')][0])
 p=d['phase_ms_per_launch']; s=d['phase_ms_per_launch_solo']
-print('$v rep=$rep', d['value'], d['median_ms_per_step'], d['value_mean'], {k: (round(s[k]*1e3), round(p[k]*1e3)) for k in ('render_fwd','render_bwd','gauss_bwd','bin_emit')})"
+print('$v rep=$rep', d['value'], d['median_ms_per_step'], d['value_mean'], {k: (round(s[k]*1e3), round(p[k]*1e3)) for k in '${PHASES:-render_fwd render_bwd gauss_bwd bin_emit}'.split()})"
   done
 done
