@@ -49,6 +49,19 @@ def test_host_only_entry_points():
     assert all(o % 256 == 0 for o in offs)
 
 
+def test_binning_bytes_follow_segment_length():
+    """gsr_binning_bytes(K, P) (ABI 16) sizes the backward's saved blend states for the segment length
+    of a P-Gaussian cloud (seg_log2, gsr_common.h): 64 list entries below 262144 Gaussians, 128 below
+    524288, 256 above, one 256-pixel float4 state per segment boundary."""
+    L = _C.load_library()
+    K = 4_000_000
+    b = {P: L.gsr_binning_bytes(K, P) for P in (262_143, 262_144, 524_287, 524_288, 2_000_000)}
+    states = lambda seg: (K // seg + 1) * 256 * 16  # noqa: E731
+    assert b[262_143] - b[262_144] == states(64) - states(128)
+    assert b[524_287] - b[524_288] == states(128) - states(256)
+    assert b[262_144] == b[524_287] and b[524_288] == b[2_000_000]
+
+
 def _cam_gauss(**kw):
     dummy = ctypes.c_void_p(0x1000)  # never dereferenced: validation fails first
     cam = _C._Camera(64, 48, 0.5, 0.5, dummy, dummy, dummy, dummy, 0)
