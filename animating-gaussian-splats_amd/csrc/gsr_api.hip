@@ -11,6 +11,8 @@
 #include <cmath>
 #include <cstring>
 #include <chrono>
+#include <condition_variable>
+#include <thread>
 #include <map>
 #include <memory>
 #include <unordered_map>
@@ -295,25 +297,253 @@ struct SpecKeyHash {
         return ((size_t)k.dev * 1000003u) ^ ((size_t)k.P * 2654435761u) ^ ((size_t)k.W << 20) ^ (size_t)k.H;
     }
 };
-struct SpecStat { uint32_t max_k = 0; bool long_lists = false; };
+// The capacity follows the largest K of the last kSpecWindow forwards of the key (one dense close-up
+// view does not inflate every later view's BINNING for good), and the table keeps the kSpecKeys most
+// recently used keys (densification changes P, i.e. the key, every 100 iterations).
+constexpr int kSpecWindow = 16;
+constexpr size_t kSpecKeys = 64;
+struct SpecStat {
+    uint32_t recent[kSpecWindow] = {};
+    int n = 0;
+    bool long_lists = false;
+    uint64_t used = 0;
+    uint32_t window_max() const {
+        uint32_t m = 0;
+        for (int k = 0; k < std::min(n, kSpecWindow); ++k) m = std::max(m, recent[k]);
+        return m;
+    }
+};
 std::mutex g_spec_mu;
 std::unordered_map<SpecKey, SpecStat, SpecKeyHash> g_spec;
-int g_spec_hits = 0, g_spec_misses = 0;
+uint64_t g_spec_clock = 0;
+int g_spec_hits = 0, g_spec_misses = 0, g_async_calls = 0;
 
 uint32_t spec_capacity(const SpecKey &key) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     auto it = g_spec.find(key);
     if (it == g_spec.end() || it->second.long_lists) return 0;
-    const uint64_t c = (uint64_t)it->second.max_k + it->second.max_k / 4 + 65536;
+    it->second.used = ++g_spec_clock;
+    const uint32_t mk = it->second.window_max();
+    const uint64_t c = (uint64_t)mk + mk / 4 + 65536;
     return (uint32_t)std::min<uint64_t>((c + 4095) & ~uint64_t(4095), 0x7FFFFFFFu);
 }
 void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
+    if (!g_spec.count(key) && g_spec.size() >= kSpecKeys) {  // evict the least recently used key
+        auto lru = g_spec.begin();
+        for (auto it = g_spec.begin(); it != g_spec.end(); ++it)
+            if (it->second.used < lru->second.used) lru = it;
+        g_spec.erase(lru);
+    }
     SpecStat &st = g_spec[key];
-    st.max_k = std::max(st.max_k, K);
+    st.recent[st.n % kSpecWindow] = K;
+    ++st.n;
     st.long_lists = long_lists;
+    st.used = ++g_spec_clock;
     if (outcome > 0) ++g_spec_hits;
     if (outcome < 0) ++g_spec_misses;
+}
+
+// ---- asynchronous forwards (ABI 17, gsr_forward_async) ------------------------------------------
+// A speculative forward whose capacity came from the key's history returns as soon as its kernels are
+// queued, without reading num_rendered back.  Each such forward takes a slot of a host-mapped ring:
+// k_bin_scan publishes K and the list-class counts into the slot's words, and the last kernel of the
+// forward, k_fwd_gate, holds the caller's stream only when the device found the capacity too small.
+// The resolver thread (one per process, no Python, no caller locks) reads every pending slot; on a
+// failed speculation it redoes the post-scan kernels exactly on its own stream, into a BINNING buffer
+// it allocates stream-ordered (hipMallocAsync), and then opens the gate.  Outputs are therefore the
+// exact path's in every case, and nothing downstream of the forward can run before they are final.
+// gsr_forward_resolve gives the backward the pair count and the BINNING buffer to use; a forward's
+// record (and the resolver's buffer, freed stream-ordered on the forward's stream) is dropped once
+// the caller released it and it is resolved.
+constexpr int kAsyncSlots = 4096;
+constexpr int kSlotWords = 16;  // 64 bytes: [0..3] k_bin_scan's host words, [4] the gate
+constexpr int kGateWord = 4;
+
+struct AsyncFwd {
+    uint64_t id = 0;
+    int dev = 0, slot = -1, T = 0;
+    hipStream_t s = nullptr;
+    uint32_t seq = 0, cap = 0;
+    bool prep = false, released = false;
+    SpecKey key{0, 0, 0, 0};
+    FwdArgs a;                  // the launch arguments (GEOM / IMAGE / outputs carved)
+    void *spec_bin = nullptr;   // the caller's BINNING, laid out for `cap`
+    hipEvent_t ev_scan = nullptr;  // recorded on `s` after k_bin_scan (the redo waits for it)
+    int state = 0;              // 0 pending, 1 stood, 2 redo queued, 3 redone, -1 failed
+    uint32_t polls = 0;
+    uint32_t K = 0;
+    int layout = 0;
+    void *bin = nullptr;        // the BINNING buffer the backward uses
+    void *own = nullptr;        // the resolver's allocation (redone forwards)
+    std::string err;
+};
+
+std::mutex g_as_mu;
+std::condition_variable g_as_wake;  // the resolver: a forward was queued / a redo is needed
+std::condition_variable g_as_done;  // resolutions
+std::unordered_map<uint64_t, std::shared_ptr<AsyncFwd>> g_as;
+uint64_t g_as_next_id = 1;
+uint32_t g_as_seq = 0;
+uint32_t *g_slot_h = nullptr, *g_slot_d = nullptr;  // kAsyncSlots * kSlotWords words + 16 (error words)
+std::vector<uint8_t> g_slot_busy;
+int g_slot_next = 0;
+std::string g_async_err;  // a failed redo or gate, reported by the next call
+bool g_resolver_started = false;
+
+uint32_t *slot_h(int k) { return g_slot_h + (size_t)k * kSlotWords; }
+uint32_t *slot_d(int k) { return g_slot_d + (size_t)k * kSlotWords; }
+uint32_t *gate_err_h() { return g_slot_h + (size_t)kAsyncSlots * kSlotWords; }
+uint32_t *gate_err_d() { return g_slot_d + (size_t)kAsyncSlots * kSlotWords; }
+
+void resolver_main();
+
+// (g_as_mu held) the slot ring and the resolver thread, on first use
+bool async_init() {
+    if (!g_slot_h) {
+        uint32_t *h = nullptr;
+        const size_t bytes = sizeof(uint32_t) * ((size_t)kAsyncSlots * kSlotWords + 16);
+        if (hipHostMalloc((void **)&h, bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+            return false;
+        uint32_t *d = nullptr;
+        if (hipHostGetDevicePointer((void **)&d, h, 0) != hipSuccess) { (void)hipHostFree(h); return false; }
+        memset(h, 0, bytes);
+        g_slot_h = h; g_slot_d = d;
+        g_slot_busy.assign(kAsyncSlots, 0);
+    }
+    if (!g_resolver_started) {
+        std::thread(resolver_main).detach();  // lives for the process; holds no caller resources
+        g_resolver_started = true;
+    }
+    return true;
+}
+
+// (g_as_mu held) a free slot, or -1 when every slot has an unresolved forward
+int slot_acquire() {
+    for (int k = 0; k < kAsyncSlots; ++k) {
+        const int j = (g_slot_next + k) % kAsyncSlots;
+        if (!g_slot_busy[j]) {
+            g_slot_busy[j] = 1;
+            g_slot_next = (j + 1) % kAsyncSlots;
+            return j;
+        }
+    }
+    return -1;
+}
+
+// (g_as_mu held) classify a forward whose K is published: 1 = the queued kernels stood, 2 = redo needed
+void async_classify(AsyncFwd &f) {
+    const uint32_t *w = slot_h(f.slot);
+    f.K = __atomic_load_n(w, __ATOMIC_ACQUIRE);
+    const uint32_t n_vlong = __atomic_load_n(w + 2, __ATOMIC_ACQUIRE);
+    if (f.K <= f.cap && n_vlong == 0) {  // the device's verdict (k_bin_scan: K <= cap, no merge-sorted list)
+        f.state = 1;
+        f.layout = (int)f.cap;
+        f.bin = f.spec_bin;
+        spec_record(f.key, f.K, false, +1);
+    } else {
+        f.state = 2;
+        spec_record(f.key, f.K, n_vlong > 0, -1);
+    }
+}
+
+// (g_as_mu held) drop a released, resolved record: the resolver's BINNING is freed stream-ordered on
+// the forward's stream (after everything the caller queued there, the backward included)
+void async_reap(std::unordered_map<uint64_t, std::shared_ptr<AsyncFwd>>::iterator it) {
+    AsyncFwd &f = *it->second;
+    if (f.own) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != f.dev) (void)hipSetDevice(f.dev);
+        (void)hipFreeAsync(f.own, f.s);
+        if (cur != f.dev) (void)hipSetDevice(cur);
+        f.own = nullptr;
+    }
+    if (f.ev_scan) (void)hipEventDestroy(f.ev_scan);
+    f.ev_scan = nullptr;
+    if (f.slot >= 0) g_slot_busy[f.slot] = 0;
+    g_as.erase(it);
+}
+
+// The exact post-scan kernels of a failed speculation, on the resolver's stream of the forward's
+// device, then the gate opens.  Runs without g_as_mu.
+int async_redo(AsyncFwd &f, std::map<int, hipStream_t> &streams) {
+    (void)hipSetDevice(f.dev);
+    hipStream_t &H = streams[f.dev];
+    if (!H) HIP_TRY(hipStreamCreateWithFlags(&H, hipStreamNonBlocking));
+    HIP_TRY(hipStreamWaitEvent(H, f.ev_scan, 0));
+    const uint32_t *w = slot_h(f.slot);
+    const uint32_t K = f.K, n_mid = w[1], n_vlong = w[2], max_n = w[3];
+    FwdArgs a = f.a;
+    a.spec_ok = nullptr;
+    a.spec_cap = 0;
+    const size_t bin_bytes = BinningLayout((int)K, a.P).total;
+    const size_t item_bytes = (GSR_FWD_ITEMS && f.prep) ? bwd_items_bytes((int)K, f.T) : 0;
+    const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
+    void *bin = nullptr;
+    if (hipMallocAsync(&bin, bin_bytes + item_bytes + tmp_bytes, H) != hipSuccess || !bin)
+        return fail(GSR_ERR_ALLOC, "asynchronous forward: hipMallocAsync of %zu bytes failed", bin_bytes + item_bytes + tmp_bytes);
+    f.own = bin;
+    carve_binning(a, (char *)bin, (int)K);
+    HIP_TRY(launch_bin_emit(a, (int)K, H));
+    HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)((char *)bin + bin_bytes + item_bytes), H));
+    HIP_TRY(launch_render_fwd(a, H));
+    if (GSR_FWD_ITEMS && f.prep)
+        HIP_TRY(launch_bwd_items_raw((int)K, f.T, a.P, a.ranges, a.tile_maxc, (uint2 *)((char *)bin + bin_bytes), H));
+    HIP_TRY(hipStreamSynchronize(H));
+    f.bin = bin;
+    f.layout = (int)K;
+    return GSR_OK;
+}
+
+void resolver_main() {
+    std::map<int, hipStream_t> streams;
+    std::unique_lock<std::mutex> lk(g_as_mu);
+    for (;;) {
+        bool pending = false, resolved = false;
+        std::shared_ptr<AsyncFwd> todo;
+        for (auto it = g_as.begin(); it != g_as.end();) {
+            AsyncFwd &f = *it->second;
+            if (f.state == 0 && __atomic_load_n(slot_h(f.slot), __ATOMIC_ACQUIRE) != kNoValue) {
+                async_classify(f);
+                resolved = resolved || f.state == 1;
+            }
+            if (f.state == 0) {
+                pending = true;
+                if (++f.polls % 20 == 0) {  // ~1 ms: a faulted stream never publishes K
+                    (void)hipSetDevice(f.dev);
+                    const hipError_t q = hipStreamQuery(f.s);
+                    if (q != hipErrorNotReady && __atomic_load_n(slot_h(f.slot), __ATOMIC_ACQUIRE) == kNoValue) {
+                        f.state = -1;
+                        f.err = q == hipSuccess ? std::string("num_rendered was not published")
+                                                : std::string("stream error before num_rendered was published: ") + hipGetErrorString(q);
+                        __atomic_store_n(slot_h(f.slot) + kGateWord, f.seq, __ATOMIC_RELEASE);
+                        resolved = true;
+                    }
+                }
+            }
+            if (f.state == 2 && !todo) todo = it->second;
+            if (f.released && (f.state == 1 || f.state == 3 || f.state == -1)) {
+                async_reap(it++);
+                continue;
+            }
+            ++it;
+        }
+        if (resolved) g_as_done.notify_all();
+        if (todo) {
+            lk.unlock();
+            const int rc = async_redo(*todo, streams);
+            const std::string msg = rc ? g_err : std::string();
+            __atomic_store_n(slot_h(todo->slot) + kGateWord, todo->seq, __ATOMIC_RELEASE);  // open the gate
+            lk.lock();
+            todo->state = rc ? -1 : 3;
+            if (rc) { todo->err = msg; g_async_err = "asynchronous forward redo failed: " + msg; }
+            g_as_done.notify_all();
+            continue;
+        }
+        if (pending) g_as_wake.wait_for(lk, std::chrono::microseconds(50));
+        else g_as_wake.wait(lk);
+    }
 }
 
 }  // namespace
@@ -329,14 +559,22 @@ extern "C" size_t gsr_spec_binning_bytes(int P, int W, int H, int prepare_backwa
 }
 
 namespace {
+// mode 0: exact (the host reads K, then queues the rest); 1: speculative, the call still returns after
+// K is known; 2: asynchronous (gsr_forward_async) -- with a capacity the call returns once everything
+// is queued, info->pending names the forward for gsr_forward_resolve / gsr_forward_release.
 int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
-                 float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, bool speculate,
+                 float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, int mode,
                  void *stream) {
     HostPhase host_total("host_forward");
     int rc = check_common(cam, g, true);
     if (rc) return rc;
     if (!alloc || !out_color || !out_depth || !info || (g->P > 0 && !out_radii))
         return fail(GSR_ERR_ARG, "gsr_forward: missing output or allocator");
+    {
+        std::lock_guard<std::mutex> lk(g_as_mu);
+        if (!g_async_err.empty()) return fail(GSR_ERR_HIP, "%s", g_async_err.c_str());
+        if (g_slot_h && gate_err_h()[0]) return fail(GSR_ERR_HIP, "an asynchronous forward's gate timed out (seq %u)", gate_err_h()[0]);
+    }
     hipStream_t s = (hipStream_t)stream;
     FwdArgs a;
     fill_common(a, cam, g);
@@ -351,6 +589,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     info->num_rendered = 0;
     info->binning_layout = 0;
     info->speculated = 0;
+    info->pending = 0;
     if (a.P == 0) {  // reference: colour/depth stay zero (no background) when there are no Gaussians
         HIP_TRY(launch_zero(out_color, 3 * npix, s));
         HIP_TRY(launch_zero(out_depth, npix, s));
@@ -361,29 +600,84 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     int dev = 0;
     (void)hipGetDevice(&dev);
     const SpecKey key{dev, a.P, a.W, a.H};
-    const uint32_t cap = speculate ? spec_capacity(key) : 0u;
+    const uint32_t cap = mode ? spec_capacity(key) : 0u;
     a.spec_cap = cap;
     const int T = a.gx * a.gy;
+    // where k_bin_scan publishes K: an asynchronous forward's ring slot, else this thread's word
+    std::shared_ptr<AsyncFwd> af;
+    uint32_t *words_h = nullptr, *words_d = nullptr;
+    if (mode == 2 && cap) {
+        std::lock_guard<std::mutex> lk(g_as_mu);
+        if (async_init()) {
+            const int slot = slot_acquire();
+            if (slot >= 0) {
+                af = std::make_shared<AsyncFwd>();
+                af->slot = slot;
+                words_h = slot_h(slot);
+                words_d = slot_d(slot);
+            }
+        }
+    }
+    struct SlotGuard {  // an acquired slot goes back to the ring unless the forward got registered
+        std::shared_ptr<AsyncFwd> *f;
+        ~SlotGuard() {
+            if (!*f || (*f)->id) return;
+            std::lock_guard<std::mutex> lk(g_as_mu);
+            g_slot_busy[(*f)->slot] = 0;
+            if ((*f)->ev_scan) (void)hipEventDestroy((*f)->ev_scan);
+        }
+    } slot_guard{&af};
+    if (!af) {
+        HostWord hw = pinned_word();
+        if (!hw.h) return fail(GSR_ERR_HIP, "hipHostMalloc(mapped) failed");
+        words_h = hw.h;
+        words_d = hw.d;
+    }
+    __atomic_store_n(words_h, kNoValue, __ATOMIC_SEQ_CST);
     { Phase ph(s, "preprocess"); HIP_TRY(launch_preprocess(a, s)); }
     { Phase ph(s, "bin_count"); HIP_TRY(launch_bin_count(a, s)); }
-    HostWord hw = pinned_word();
-    if (!hw.h) return fail(GSR_ERR_HIP, "hipHostMalloc(mapped) failed");
-    __atomic_store_n(hw.h, kNoValue, __ATOMIC_SEQ_CST);
-    { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, hw.d, s)); }
+    { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, words_d, s)); }
+    if (af) {
+        HIP_TRY(hipEventCreateWithFlags(&af->ev_scan, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(af->ev_scan, s));
+    }
     const size_t spec_item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;
+    char *spec_bin = nullptr;
     if (cap) {  // speculative: the post-scan kernels are queued now, against the capacity
-        char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)cap, a.P).total + spec_item_bytes);
-        if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, capacity %u)", cap);
-        carve_binning(a, bin, (int)cap);
-        a.spec_ok = a.meta + 1;
-        { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, 0, s)); }
-        { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, 0, 0, 0, nullptr, s)); }
-        { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
+        spec_bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)cap, a.P).total + spec_item_bytes);
+        if (!spec_bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, capacity %u)", cap);
+        FwdArgs sa = a;
+        carve_binning(sa, spec_bin, (int)cap);
+        sa.spec_ok = sa.meta + 1;
+        { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(sa, 0, s)); }
+        { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(sa, 0, 0, 0, nullptr, s)); }
+        { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(sa, s)); }
         if (GSR_FWD_ITEMS && g->prepare_backward) {
             Phase ph(s, "bwd_items");
             HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc,
-                                         (uint2 *)(bin + BinningLayout((int)cap, a.P).total), s, a.spec_ok));
+                                         (uint2 *)(spec_bin + BinningLayout((int)cap, a.P).total), s, sa.spec_ok));
         }
+    }
+    if (af) {  // asynchronous: gate the stream on the verdict and return
+        std::lock_guard<std::mutex> lk(g_as_mu);
+        af->id = g_as_next_id++;
+        af->seq = ++g_as_seq;
+        af->dev = dev; af->s = s; af->cap = cap; af->T = T; af->key = key;
+        af->prep = g->prepare_backward != 0;
+        af->a = a;
+        af->spec_bin = spec_bin;
+        HIP_TRY(launch_fwd_gate(a.meta + 1, words_d + kGateWord, af->seq, gate_err_d(), s));
+        g_as[af->id] = af;
+        info->num_rendered = -1;
+        info->binning_layout = (int)cap;
+        info->speculated = 1;
+        info->pending = af->id;
+        {
+            std::lock_guard<std::mutex> lk2(g_spec_mu);
+            ++g_async_calls;
+        }
+        g_as_wake.notify_one();
+        return GSR_OK;
     }
     uint32_t K;
     {
@@ -392,14 +686,14 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         // stream, so this can take milliseconds).  Every ~0.5 ms ask the runtime whether the stream
         // has drained or failed, so a faulted launch cannot leave us spinning.
         auto last = hclock::now();
-        while ((K = __atomic_load_n(hw.h, __ATOMIC_ACQUIRE)) == kNoValue) {
+        while ((K = __atomic_load_n(words_h, __ATOMIC_ACQUIRE)) == kNoValue) {
             __builtin_ia32_pause();
             if (hclock::now() - last > std::chrono::microseconds(500)) {
                 last = hclock::now();
                 const hipError_t q = hipStreamQuery(s);
                 if (q == hipErrorNotReady) continue;
                 if (q != hipSuccess) return fail(GSR_ERR_HIP, "stream error while waiting for num_rendered: %s", hipGetErrorString(q));
-                K = __atomic_load_n(hw.h, __ATOMIC_ACQUIRE);
+                K = __atomic_load_n(words_h, __ATOMIC_ACQUIRE);
                 if (K == kNoValue) return fail(GSR_ERR_HIP, "num_rendered was not published");
                 break;
             }
@@ -409,9 +703,9 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     info->num_rendered = (int)K;
     // tiles to sort outside the render: [1] up to kSortCap pairs, [2] longer (merge sort), [3] the
     // longest list (merge passes); the latter need a temporary copy of the pair records
-    const uint32_t n_mid = __atomic_load_n(hw.h + 1, __ATOMIC_ACQUIRE);
-    const uint32_t n_vlong = __atomic_load_n(hw.h + 2, __ATOMIC_ACQUIRE);
-    const uint32_t max_n = __atomic_load_n(hw.h + 3, __ATOMIC_ACQUIRE);
+    const uint32_t n_mid = __atomic_load_n(words_h + 1, __ATOMIC_ACQUIRE);
+    const uint32_t n_vlong = __atomic_load_n(words_h + 2, __ATOMIC_ACQUIRE);
+    const uint32_t max_n = __atomic_load_n(words_h + 3, __ATOMIC_ACQUIRE);
     if (cap && K <= cap && n_vlong == 0) {  // the device took the same verdict: the queued work stands
         info->binning_layout = (int)cap;
         info->speculated = 1;
@@ -448,7 +742,7 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
     if (!out_num_rendered) return fail(GSR_ERR_ARG, "gsr_forward: missing output or allocator");
     *out_num_rendered = 0;
     gsr_forward_info info;
-    const int rc = forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, &info, false, stream);
+    const int rc = forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, &info, 0, stream);
     *out_num_rendered = info.num_rendered;
     return rc;
 }
@@ -457,15 +751,107 @@ int gsr_forward_info_call(const gsr_camera *cam, const gsr_gaussians *g, gsr_all
                           float *out_color, float *out_depth, int *out_radii, int speculate, gsr_forward_info *info,
                           void *stream) {
     if (!info) return fail(GSR_ERR_ARG, "gsr_forward_info_call: null info");
-    return forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, info, speculate != 0, stream);
+    return forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, info, speculate ? 1 : 0, stream);
+}
+
+int gsr_forward_async(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                      float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, void *stream) {
+    if (!info) return fail(GSR_ERR_ARG, "gsr_forward_async: null info");
+    return forward_impl(cam, g, alloc, alloc_ctx, out_color, out_depth, out_radii, info, 2, stream);
+}
+
+int gsr_forward_resolve(unsigned long long handle, gsr_forward_resolution *out) {
+    if (!out) return fail(GSR_ERR_ARG, "gsr_forward_resolve: null output");
+    HostPhase hp("host_wait_K");
+    std::unique_lock<std::mutex> lk(g_as_mu);
+    auto it = g_as.find(handle);
+    if (it == g_as.end()) return fail(GSR_ERR_ARG, "gsr_forward_resolve: unknown or released forward %llu", handle);
+    std::shared_ptr<AsyncFwd> f = it->second;
+    auto last = hclock::now();
+    while (f->state == 0 || f->state == 2) {
+        if (f->state == 0) {
+            if (__atomic_load_n(slot_h(f->slot), __ATOMIC_ACQUIRE) != kNoValue) {
+                async_classify(*f);
+                if (f->state == 2) g_as_wake.notify_one();  // the resolver redoes it
+                continue;
+            }
+            // K not published yet: spin outside the lock, checking the stream for faults every ~0.5 ms
+            lk.unlock();
+            while (__atomic_load_n(slot_h(f->slot), __ATOMIC_ACQUIRE) == kNoValue) {
+                __builtin_ia32_pause();
+                if (hclock::now() - last > std::chrono::microseconds(500)) {
+                    last = hclock::now();
+                    const hipError_t q = hipStreamQuery(f->s);
+                    if (q == hipErrorNotReady) continue;
+                    if (__atomic_load_n(slot_h(f->slot), __ATOMIC_ACQUIRE) != kNoValue) break;
+                    lk.lock();
+                    if (f->state == 0) {
+                        f->state = -1;
+                        f->err = q == hipSuccess ? std::string("num_rendered was not published")
+                                                 : std::string("stream error: ") + hipGetErrorString(q);
+                        __atomic_store_n(slot_h(f->slot) + kGateWord, f->seq, __ATOMIC_RELEASE);
+                    }
+                    lk.unlock();
+                    break;
+                }
+            }
+            lk.lock();
+            continue;
+        }
+        g_as_done.wait(lk);
+    }
+    if (f->state < 0) return fail(GSR_ERR_HIP, "asynchronous forward %llu failed: %s", handle, f->err.c_str());
+    out->num_rendered = (int)f->K;
+    out->binning_layout = f->layout;
+    out->binning = f->bin;
+    out->redone = f->state == 3;
+    return GSR_OK;
+}
+
+int gsr_forward_query(unsigned long long handle) {
+    std::lock_guard<std::mutex> lk(g_as_mu);
+    auto it = g_as.find(handle);
+    if (it == g_as.end()) return -1;
+    AsyncFwd &f = *it->second;
+    if (f.state == 0 && __atomic_load_n(slot_h(f.slot), __ATOMIC_ACQUIRE) != kNoValue) {
+        async_classify(f);
+        if (f.state == 2) g_as_wake.notify_one();
+    }
+    return (f.state == 1 || f.state == 3 || f.state == -1) ? 1 : 0;
+}
+
+int gsr_forward_release(unsigned long long handle) {
+    std::lock_guard<std::mutex> lk(g_as_mu);
+    auto it = g_as.find(handle);
+    if (it == g_as.end()) return GSR_OK;
+    it->second->released = true;
+    const int st = it->second->state;
+    if (st == 1 || st == 3 || st == -1) async_reap(it);
+    else g_as_wake.notify_one();  // reaped by the resolver once resolved
+    return GSR_OK;
+}
+
+int gsr_async_stats(int *calls, int *pending) {
+    {
+        std::lock_guard<std::mutex> lk(g_spec_mu);
+        if (calls) *calls = g_async_calls;
+    }
+    std::lock_guard<std::mutex> lk(g_as_mu);
+    if (pending) *pending = (int)g_as.size();
+    return GSR_OK;
 }
 
 int gsr_spec_stats(int *hits, int *misses, int reset) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     if (hits) *hits = g_spec_hits;
     if (misses) *misses = g_spec_misses;
-    if (reset) { g_spec.clear(); g_spec_hits = g_spec_misses = 0; }
+    if (reset) { g_spec.clear(); g_spec_hits = g_spec_misses = g_async_calls = 0; }
     return GSR_OK;
+}
+
+int gsr_spec_keys(void) {
+    std::lock_guard<std::mutex> lk(g_spec_mu);
+    return (int)g_spec.size();
 }
 
 }  // extern "C"

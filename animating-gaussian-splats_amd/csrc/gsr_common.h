@@ -578,6 +578,10 @@ __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha
 // lowered by a no-return ds_and, was then read stale by other waves after the barrier: waves of one
 // block left the loop at different batches, the tile's quarter maxima were corrupted and the backward
 // went nondeterministic).  An explicit wait is kept by the compiler.
+// tools/lds_lint.py (tests/test_lds_lint.py) checks every barrier of the shipped code object for the wait.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "lds_barrier(): 0xC07F is the gfx9 s_waitcnt encoding (lgkmcnt(0)); pick the target's encoding"
+#endif
 __device__ inline void lds_barrier() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // gfx9 encoding: vmcnt / expcnt at maximum, lgkmcnt(0)
     __syncthreads();

@@ -338,7 +338,7 @@ __global__ __launch_bounds__(1024) void k_bin_scan(int T, int NB, const uint32_t
             sort_lists[atomicAdd(&s_cls[0], 1u)] = (uint32_t)t;
         }
     }
-    __syncthreads();
+    lds_barrier();  // s_cls: no-return LDS atomics above
     if (threadIdx.x == 0) {
         meta[0] = carry;
         meta[1] = (cap && carry <= cap && s_cls[1] == 0u) ? 1u : 0u;
@@ -856,7 +856,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     if (threadIdx.x < 4) s_u.st.q[threadIdx.x] = 0;
     __syncthreads();
     if ((lane & 31) == 0) atomicMax(&s_u.st.q[2 * (wv >> 1) + (lane >> 5)], mx);
-    __syncthreads();
+    lds_barrier();  // the quarter maxima: no-return LDS atomics
     if (threadIdx.x < 4) tile_maxc[4 * tile + threadIdx.x] = s_u.st.q[threadIdx.x];
 #else
     uint32_t mx = last;
@@ -867,6 +867,27 @@ __global__ __launch_bounds__(256) void k_render_fwd(
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
 #endif
+}
+
+// The end of an asynchronous forward (gsr_forward_async): when k_bin_scan found the speculative
+// capacity too small (spec_ok == 0: the queued kernels returned at once), hold this stream until the
+// library's resolver thread has redone the post-scan kernels exactly on its own stream and published
+// `seq` in the slot's gate word (host-mapped).  Everything the caller queues after the forward is
+// ordered behind this one-wave kernel; when the speculation stood it returns at once.  A gate that
+// never opens (the resolver died) is abandoned after kGateTimeoutTicks with an error word set, so a
+// failure cannot hang the device.
+constexpr uint64_t kGateTimeoutTicks = 2000000000ull;  // s_memrealtime runs at 100 MHz: 20 s
+__global__ __launch_bounds__(64) void k_fwd_gate(const uint32_t *__restrict__ spec_ok, const uint32_t *gate,
+                                                 uint32_t seq, uint32_t *err) {
+    if (*spec_ok) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+        __builtin_amdgcn_s_sleep(100);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+            if (threadIdx.x == 0) __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+    }
 }
 
 __global__ void k_zero_f32(float *p, size_t n) {
@@ -976,6 +997,11 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                                    a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
                                    a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P));
+    return hipGetLastError();
+}
+
+hipError_t launch_fwd_gate(const uint32_t *spec_ok, const uint32_t *gate, uint32_t seq, uint32_t *err, hipStream_t s) {
+    k_fwd_gate<<<1, 64, 0, s>>>(spec_ok, gate, seq, err);
     return hipGetLastError();
 }
 

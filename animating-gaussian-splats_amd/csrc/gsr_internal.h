@@ -61,6 +61,8 @@ hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, 
                             hipStream_t s);
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s);
 hipError_t launch_zero(float *p, size_t n, hipStream_t s);
+// asynchronous forward: holds the stream until a failed speculation has been redone (gsr_api.hip)
+hipError_t launch_fwd_gate(const uint32_t *spec_ok, const uint32_t *gate, uint32_t seq, uint32_t *err, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 

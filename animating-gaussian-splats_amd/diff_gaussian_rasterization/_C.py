@@ -38,6 +38,8 @@ EXPORTED_SYMBOLS = (
     "gsr_densify_plan", "gsr_densify_split_stds", "gsr_densify_apply", "gsr_adam_step", "gsr_views_pack",
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
     "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes", "gsr_prealloc_alloc", "gsr_spec_binning_bytes",
+    "gsr_forward_async", "gsr_forward_resolve", "gsr_forward_release", "gsr_forward_query", "gsr_async_stats",
+    "gsr_spec_keys",
 )
 
 
@@ -60,8 +62,14 @@ class _Gaussians(ctypes.Structure):
                 ("binning_layout", ctypes.c_int)]
 
 
-class _ForwardInfo(ctypes.Structure):  # gsr_forward_info (ABI 14)
-    _fields_ = [("num_rendered", ctypes.c_int), ("binning_layout", ctypes.c_int), ("speculated", ctypes.c_int)]
+class _ForwardInfo(ctypes.Structure):  # gsr_forward_info (ABI 17)
+    _fields_ = [("num_rendered", ctypes.c_int), ("binning_layout", ctypes.c_int), ("speculated", ctypes.c_int),
+                ("pending", ctypes.c_ulonglong)]
+
+
+class _Resolution(ctypes.Structure):  # gsr_forward_resolution (ABI 17)
+    _fields_ = [("num_rendered", ctypes.c_int), ("binning_layout", ctypes.c_int), ("binning", ctypes.c_void_p),
+                ("redone", ctypes.c_int)]
 
 
 class _Grads(ctypes.Structure):
@@ -107,6 +115,19 @@ def load_library():
                                         vp, vp, vp, i, ctypes.POINTER(_ForwardInfo), vp]
     L.gsr_spec_stats.restype = i
     L.gsr_spec_stats.argtypes = [ctypes.POINTER(i), ctypes.POINTER(i), i]
+    L.gsr_spec_keys.restype = i
+    L.gsr_spec_keys.argtypes = []
+    L.gsr_forward_async.restype = i
+    L.gsr_forward_async.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), _ALLOC_FN, vp,
+                                    vp, vp, vp, ctypes.POINTER(_ForwardInfo), vp]
+    L.gsr_forward_resolve.restype = i
+    L.gsr_forward_resolve.argtypes = [ctypes.c_ulonglong, ctypes.POINTER(_Resolution)]
+    L.gsr_forward_release.restype = i
+    L.gsr_forward_release.argtypes = [ctypes.c_ulonglong]
+    L.gsr_forward_query.restype = i
+    L.gsr_forward_query.argtypes = [ctypes.c_ulonglong]
+    L.gsr_async_stats.restype = i
+    L.gsr_async_stats.argtypes = [ctypes.POINTER(i), ctypes.POINTER(i)]
     L.gsr_backward.restype = i
     L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
                                vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]
@@ -159,7 +180,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 16  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 17  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -317,17 +338,60 @@ def _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_mo
                       int(activations), int(bool(prepare_backward)), int(binning_layout or 0)), P, M
 
 
+class AsyncForward:
+    """An asynchronous forward's handle (gsr_forward_async): ``resolve()`` waits until its pair count is
+    known and returns ``(num_rendered, binning_layout, binning_ptr)`` -- what the backward calls take
+    (the BINNING buffer is the forward's own, or the library's when the speculation was redone);
+    ``ready()`` says whether that would return without waiting.  The handle is released when this
+    object is collected (after the backward that holds it)."""
+    __slots__ = ("handle", "_res", "__weakref__")
+
+    def __init__(self, handle):
+        self.handle = int(handle)
+        self._res = None
+        import weakref
+        weakref.finalize(self, _release_async, self.handle)
+
+    def ready(self):
+        return self._res is not None or load_library().gsr_forward_query(self.handle) > 0
+
+    def resolve(self):
+        if self._res is None:
+            r = _Resolution()
+            _check(load_library().gsr_forward_resolve(self.handle, ctypes.byref(r)))
+            self._res = (r.num_rendered, r.binning_layout, r.binning, bool(r.redone))
+        return self._res[:3]
+
+    @property
+    def redone(self):
+        return self._res[3] if self._res is not None else None
+
+
+def _release_async(handle):
+    if _lib is not None:
+        _lib.gsr_forward_release(handle)
+
+
+def async_stats():
+    """(asynchronous forwards since the last speculation_stats(reset=True), handles still held)."""
+    c, p = ctypes.c_int(0), ctypes.c_int(0)
+    _check(load_library().gsr_async_stats(ctypes.byref(c), ctypes.byref(p)))
+    return c.value, p.value
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
                         image_width, sh, degree, campos, prefiltered, debug=False, activations=0,
-                        prepare_backward=False, speculate=False, info=None):
+                        prepare_backward=False, speculate=False, info=None, nonblocking=False):
     """``activations`` (ACT_* bits): opacity / scales / rotations hold the raw parameters of
     shared.py:29-42 and are activated inside the kernels (0 = the reference's interface).
     ``prepare_backward``: a backward will follow; the forward also builds its work-item list (the
     backward calls must then pass the same flag).  ``speculate``: queue the post-scan kernels before
     num_rendered is read back (gsr_forward_info_call, include/gsr.h); ``info`` (a dict) receives
-    ``num_rendered``, ``binning_layout`` (pass it to the backward calls and decode_buffers) and
-    ``speculated``."""
+    ``num_rendered``, ``binning_layout`` (pass it to the backward calls and decode_buffers),
+    ``speculated`` and ``pending``.  ``nonblocking``: gsr_forward_async -- with a capacity from the
+    pair-count history the call returns without reading num_rendered back; ``num_rendered`` is then
+    -1 and ``info["pending"]`` an ``AsyncForward`` whose ``resolve()`` gives what the backward needs."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
@@ -341,16 +405,24 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     radii = torch.empty((P,), dtype=torch.int32, device=dev)  # preprocess writes every entry
     fi = _ForwardInfo(0, 0, 0)
     with _device_guard(dev):  # launches go to dev even when another device is current
-        # GEOM, IMAGE and (when this forward will speculate) BINNING sized here, in one allocation
-        spec = L.gsr_spec_binning_bytes(P, W, H, int(bool(prepare_backward))) if speculate and P else 0
-        alloc = _PreAllocator(dev, [[(GSR_BUF_GEOM, L.gsr_geom_bytes(P)), (GSR_BUF_IMAGE, L.gsr_image_bytes(W, H, P)),
-                                     (GSR_BUF_BINNING, spec)]])
+        # GEOM + IMAGE sized here in one allocation; the speculative BINNING (when this forward will
+        # speculate) in its own, so that a failed speculation's buffer is released with the call
+        spec = L.gsr_spec_binning_bytes(P, W, H, int(bool(prepare_backward))) if (speculate or nonblocking) and P else 0
+        alloc = _PreAllocator(dev, [[(GSR_BUF_GEOM, L.gsr_geom_bytes(P)), (GSR_BUF_IMAGE, L.gsr_image_bytes(W, H, P))],
+                                    [(GSR_BUF_BINNING, spec)]])
         with alloc:
-            _check(L.gsr_forward_info_call(ctypes.byref(cam), ctypes.byref(g), alloc.cb, alloc.ctx, color.data_ptr(),
-                                           depth.data_ptr(), radii.data_ptr() if P else None, int(bool(speculate)),
-                                           ctypes.byref(fi), _stream_ptr(dev)))
+            if nonblocking:
+                _check(L.gsr_forward_async(ctypes.byref(cam), ctypes.byref(g), alloc.cb, alloc.ctx, color.data_ptr(),
+                                           depth.data_ptr(), radii.data_ptr() if P else None, ctypes.byref(fi),
+                                           _stream_ptr(dev)))
+            else:
+                _check(L.gsr_forward_info_call(ctypes.byref(cam), ctypes.byref(g), alloc.cb, alloc.ctx,
+                                               color.data_ptr(), depth.data_ptr(), radii.data_ptr() if P else None,
+                                               int(bool(speculate)), ctypes.byref(fi), _stream_ptr(dev)))
+    pending = AsyncForward(fi.pending) if fi.pending else None
     if info is not None:
-        info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated))
+        info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated),
+                    pending=pending)
     b = alloc.buffers
     return fi.num_rendered, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
 
@@ -407,7 +479,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
                                  tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                  binningBuffer, imageBuffer, debug=False, dL_dout_depth=None,
                                  activations=0, skip_unused=False, accumulate_into=None,
-                                 prepare_backward=False, needed=None, binning_layout=0):
+                                 prepare_backward=False, needed=None, binning_layout=0, binning_ptr=None):
     """Returns the 8 gradients of the upstream binding.  ``skip_unused``: gradients of inputs that
     were not given (colours under SH, cov3D under scales/rotations and vice versa) come back as
     empty tensors and their HBM writes are skipped.  ``accumulate_into``: optional sequence of 8
@@ -416,7 +488,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     returned in that slot.  ``needed``: optional 8 booleans in output order; a False slot is not
     computed into memory at all (NULL output, ABI 13) and comes back as None -- the autograd
     Function passes ``needs_input_grad`` (train.py renders frozen Gaussians: only means3D,
-    rotations and means2D need a gradient there)."""
+    rotations and means2D need a gradient there).  ``binning_ptr``: the BINNING buffer to read instead
+    of ``binningBuffer``'s (an asynchronous forward's, from ``AsyncForward.resolve()``)."""
     L = load_library()
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
@@ -436,7 +509,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     alloc = _PreAllocator(dev, [[(GSR_BUF_SCRATCH, L.gsr_scratch_bytes(int(R), W, H))]])
     with _device_guard(dev), alloc:
         _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
-                              geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+                              geomBuffer.data_ptr(), binning_ptr or binningBuffer.data_ptr(), imageBuffer.data_ptr(),
                               dpix.data_ptr(), None, alloc.cb, alloc.ctx, ctypes.byref(grads), _stream_ptr(dev)))
     return out
 
@@ -445,7 +518,7 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
                                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                         tan_fovy, dL_dout_color, sh, degree, campos, geomBuffer, R,
                                         binningBuffer, imageBuffer, activations=0, prepare_backward=False,
-                                        binning_layout=0):
+                                        binning_layout=0, binning_ptr=None):
     """The per-pixel half of ``rasterize_gaussians_backward`` (gsr_backward_render): returns the
     view's SUMS byte buffer (each Gaussian's per-(tile, Gaussian) gradient records summed, 9 x P
     floats), for ``rasterize_gaussians_backward_views``; the records' SCRATCH buffer is released here
@@ -467,7 +540,8 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
                                 [(GSR_BUF_SUMS, L.gsr_sums_bytes(P))]])
     with _device_guard(dev), alloc:
         _check(L.gsr_backward_render(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
-                                     geomBuffer.data_ptr(), binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+                                     geomBuffer.data_ptr(), binning_ptr or binningBuffer.data_ptr(),
+                                     imageBuffer.data_ptr(),
                                      dpix.data_ptr(), alloc.cb, alloc.ctx, _stream_ptr(dev)))
     return alloc.buffers[GSR_BUF_SUMS]
 

@@ -24,8 +24,8 @@ from torch.autograd.graph import get_gradient_edge
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "pending_views",
-           "clear_pending"]
+           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "set_async_forward",
+           "pending_views", "clear_pending"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -152,7 +152,10 @@ _defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0",
           "fresh": os.environ.get("GSR_FRESH_GRADS", "1") != "0",
           # forwards queue their post-scan kernels before num_rendered is read back (include/gsr.h,
           # gsr_forward_info_call): the stream does not idle while the host reads K and launches
-          "speculate": os.environ.get("GSR_SPECULATE", "1") != "0"}
+          "speculate": os.environ.get("GSR_SPECULATE", "1") != "0",
+          # forwards with a pair-count history return without reading num_rendered back
+          # (gsr_forward_async): one host thread keeps queueing views while the GPU renders
+          "async": os.environ.get("GSR_ASYNC_FORWARD", "1") != "0"}
 _pending_lock = threading.Lock()
 _pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
 _queued = set()  # graph tasks whose flush callback is queued
@@ -171,6 +174,23 @@ def set_speculative_forward(on: bool) -> bool:
     prev = _defer["speculate"]
     _defer["speculate"] = bool(on)
     return prev
+
+
+def set_async_forward(on: bool) -> bool:
+    """Enable / disable the asynchronous forward (gsr_forward_async: no host wait for num_rendered when
+    the pair-count history gives a capacity); returns the previous setting.  Outputs are bitwise the
+    same either way."""
+    prev = _defer["async"]
+    _defer["async"] = bool(on)
+    return prev
+
+
+def _resolved(ctx):
+    """(num_rendered, binning_layout, binning pointer or None) of the forward behind ``ctx``: an
+    asynchronous forward is resolved here (waits for its pair count if the GPU has not produced it)."""
+    if ctx.pending is not None:
+        return ctx.pending.resolve()
+    return ctx.num_rendered, ctx.binning_layout, None
 
 
 def pending_views() -> int:
@@ -232,6 +252,10 @@ def _run_group(grp, created, post):
     dev = grp["device"]
     with torch.cuda.device(dev):
         cur = torch.cuda.current_stream(dev)
+        for v in grp["views"]:  # render halves held back while their forward's pair count was unknown
+            if v["scratch"] is None:
+                with torch.cuda.stream(v["stream"]):
+                    v["scratch"], v["num_rendered"] = v.pop("render_fn")()
         for s in grp["streams"]:  # every view's render half precedes the per-Gaussian pass
             if s != cur:
                 cur.wait_stream(s)
@@ -261,7 +285,11 @@ def _run_group(grp, created, post):
 def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn):
     """Queue this view for the end-of-pass per-Gaussian backward when every gradient it must produce
     can go into a leaf's .grad; returns True when queued (the Function then returns None for all).
-    ``render_fn()`` runs the view's per-pixel half and returns its SCRATCH buffer."""
+    ``render_fn()`` runs the view's per-pixel half and returns ``(SUMS buffer, num_rendered)``.  When
+    the view's forward was asynchronous and its pair count is not known yet (the GPU has not reached
+    its tile scan -- the pass's first nodes belong to the step's last views), the render half is held
+    back until the end-of-pass callback instead of waiting here, so the earlier views' render halves
+    are queued first."""
     if not _defer["on"]:
         return False
     means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act = gauss
@@ -283,7 +311,11 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
             return False  # autograd must receive this gradient: immediate path
         targets[k] = tgt
     rs = ctx.raster_settings
-    scratch = render_fn()
+    stream = torch.cuda.current_stream(means3D.device)
+    if ctx.pending is None or ctx.pending.ready():
+        scratch, K = render_fn()
+    else:
+        scratch, K = None, -1
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else 0  # noqa: E731
     tkey = lambda t: ("fresh", id(t.leaf)) if isinstance(t, _Fresh) else ptr(t)  # noqa: E731
     key = (means3D.device, P, ptr(means3D), ptr(scales), ptr(rotations), ptr(cov3D), ptr(sh), ptr(colors),
@@ -291,8 +323,9 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
     view = {"viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix, "tanfovx": rs.tanfovx,
             "tanfovy": rs.tanfovy, "image_height": rs.image_height, "image_width": rs.image_width,
             "campos": rs.campos, "bg": rs.bg, "radii": radii, "geomBuffer": geomBuffer, "scratch": scratch,
-            "num_rendered": ctx.num_rendered, "means2D_grad": targets[0], "accumulate_means2D": True}
-    stream = torch.cuda.current_stream(means3D.device)
+            "num_rendered": K, "means2D_grad": targets[0], "accumulate_means2D": True, "stream": stream}
+    if scratch is None:
+        view["render_fn"] = render_fn
     with _pending_lock:
         grp = _pending.get((task, key))
         if grp is None:
@@ -327,10 +360,12 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)
         info = {}
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = \
-            _C.rasterize_gaussians(*args, prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info)
+            _C.rasterize_gaussians(*args, prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info,
+                                   nonblocking=_defer["async"])
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.binning_layout = info["binning_layout"]
+        ctx.pending = info["pending"]  # an asynchronous forward: resolved by the backward
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
         ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
         ctx.tensor_pos = _tensor_positions((means3D, means2D, sh, colors_precomp, opacities, scales,
@@ -348,17 +383,23 @@ class _RasterizeGaussians(torch.autograd.Function):
         rs = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
          binningBuffer, imgBuffer) = ctx.saved_tensors
-        args = (rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
-                cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
-                sh, rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer)
-        kw = {"prepare_backward": ctx.prep, "binning_layout": ctx.binning_layout}
+        def args_kw():  # the forward's pair count and BINNING (an asynchronous forward resolves here)
+            K, layout, bptr = _resolved(ctx)
+            return ((rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
+                     cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
+                     sh, rs.sh_degree, rs.campos, geomBuffer, K, binningBuffer, imgBuffer),
+                    {"prepare_backward": ctx.prep, "binning_layout": layout, "binning_ptr": bptr})
+
+        def render_half():
+            a, k = args_kw()
+            return _C.rasterize_gaussians_backward_render(*a, **k), a[17]
         inputs = (1, 3, 4, 0, 7, 2, 5, 6)  # input index of each leaf (grad output order)
         nodes = _input_nodes(ctx, inputs)
         gauss = (means3D, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
                  rs.sh_degree, 0)
-        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad,
-                      lambda: _C.rasterize_gaussians_backward_render(*args, **kw)):
+        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad, render_half):
             return (None,) * 10  # every gradient is added into its leaf's .grad at the end of the pass
+        args, kw = args_kw()
         need = [ctx.needs_input_grad[i] for i in inputs]
         acc = [_accumulation_target(t, node) if n else None for t, n, node in zip(ctx.leaves, need, nodes)]
         g = list(_C.rasterize_gaussians_backward(*args, skip_unused=True, accumulate_into=acc, needed=need, **kw))
@@ -441,10 +482,11 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
             rs.bg, means, colors, opacity_logits, log_scales, quaternions, rs.scale_modifier, empty,
             rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
             rs.sh_degree, rs.campos, rs.prefiltered, activations=_C.ACT_ALL,
-            prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info)
+            prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info, nonblocking=_defer["async"])
         ctx.raster_settings = rs
         ctx.num_rendered = num_rendered
         ctx.binning_layout = info["binning_layout"]
+        ctx.pending = info["pending"]
         ctx.opacity_shape = opacity_logits.shape
         ctx.leaves = (means2D, colors, opacity_logits, means, None, sh, log_scales, quaternions)
         ctx.tensor_pos = _tensor_positions((means, means2D, sh, colors, opacity_logits, log_scales, quaternions))
@@ -467,13 +509,16 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         nodes = _input_nodes(ctx, [i for i in inputs if i is not None])
         nodes.insert(4, None)
         gauss = (means, colors, log_scales, quaternions, rs.scale_modifier, empty, sh, rs.sh_degree, _C.ACT_ALL)
-        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, need,
-                      lambda: _C.rasterize_gaussians_backward_render(
-                          rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
-                          rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,
-                          rs.sh_degree, rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
-                          activations=_C.ACT_ALL, prepare_backward=ctx.prep, binning_layout=ctx.binning_layout)):
+        def render_half():
+            K, layout, bptr = _resolved(ctx)
+            return _C.rasterize_gaussians_backward_render(
+                rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
+                rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,
+                rs.sh_degree, rs.campos, geomBuffer, K, binningBuffer, imgBuffer,
+                activations=_C.ACT_ALL, prepare_backward=ctx.prep, binning_layout=layout, binning_ptr=bptr), K
+        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, need, render_half):
             return (None,) * 9
+        K, layout, bptr = _resolved(ctx)
         acc = [_accumulation_target(t, node) if i is not None and need[i] else None
                for t, i, node in zip(ctx.leaves, inputs, nodes)]
         if acc[2] is not None and acc[2].shape != (means.shape[0], 1):
@@ -483,9 +528,9 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
             _C.rasterize_gaussians_backward(
                 rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh, rs.sh_degree,
-                rs.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer,
+                rs.campos, geomBuffer, K, binningBuffer, imgBuffer,
                 activations=_C.ACT_ALL, skip_unused=True, accumulate_into=acc, prepare_backward=ctx.prep,
-                needed=needed, binning_layout=ctx.binning_layout)
+                needed=needed, binning_layout=layout, binning_ptr=bptr)
         done = [t is not None or not n for t, n in zip(acc, needed)]  # in the leaf's .grad / not needed: None
         return (None if done[3] else g_means, None if (done[0] or not need[1]) else g_means2D,
                 None if (done[5] or not sh.numel()) else g_sh,

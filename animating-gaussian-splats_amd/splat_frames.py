@@ -59,8 +59,9 @@ class FrameFits:
         self.n_frames = n_frames
         self.frames = list(splat_dp.shard_frames(n_frames, rank, world))
         self.streams = list(streams) if streams else None
-        self.main = main_stream
         dev = base["means"].device
+        # the stream the per-frame backward + Adam run on: the caller's, or the current one
+        self.main = main_stream if main_stream is not None or not self.streams else torch.cuda.current_stream(dev)
         self.phi = frame_displacement(base["means"].shape[0], dev)
         self.params, self.opts, self.targets = {}, {}, {}
         with torch.no_grad():

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 16
+#define GSR_ABI_VERSION 17
 
 enum gsr_status {
     GSR_OK = 0,
@@ -161,15 +161,48 @@ int gsr_forward(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn allo
  * is laid out for (the capacity, or num_rendered); pass it to the backward calls in
  * gsr_gaussians.binning_layout and to gsr_buffer_offsets. */
 typedef struct gsr_forward_info {
-    int num_rendered;    /* K, the reference's num_rendered */
+    int num_rendered;    /* K, the reference's num_rendered (-1: pending, see gsr_forward_async) */
     int binning_layout;  /* the pair count BINNING is laid out for (>= num_rendered) */
     int speculated;      /* 1: the speculatively queued kernels stood; 0: exact path */
+    unsigned long long pending;  /* ABI >= 17: nonzero = an asynchronous forward's handle */
 } gsr_forward_info;
 int gsr_forward_info_call(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
                           float *out_color, float *out_depth, int *out_radii, int speculate, gsr_forward_info *info,
                           void *stream);
 /* Speculation counters since the last reset (stood / redone); reset != 0 also clears the history. */
 int gsr_spec_stats(int *hits, int *misses, int reset);
+/* Pair-count history keys held (at most 64; the least recently used key is evicted). */
+int gsr_spec_keys(void);
+
+/* Asynchronous forward (ABI >= 17).  Like gsr_forward_info_call with speculation, but when the
+ * speculation has a capacity (a key with history, no long-list merge sort) the call returns as soon
+ * as every kernel is queued -- the host never waits for num_rendered, so a caller that renders
+ * several views from one thread (train.py:402-412) keeps queueing while the GPU works.  It then sets
+ * info->num_rendered = -1 and info->pending to a handle.  The device checks the capacity after the
+ * tile scan; when it did not hold, the library's resolver thread redoes the post-scan kernels with
+ * the exact pair count on a stream of its own and the forward's last kernel holds `stream` until
+ * that is done, so everything queued after the call sees the exact outputs (bitwise those of
+ * gsr_forward).  Without a capacity it behaves as gsr_forward_info_call (pending = 0).
+ *   gsr_forward_resolve  waits until the forward's pair count is known (and a redo is done) and gives
+ *                        the pair count, the BINNING layout and the BINNING buffer to hand to the
+ *                        backward calls (the caller's buffer, or the resolver's for a redone forward)
+ *   gsr_forward_release  the caller is done with the handle (after its backward, or at once for a
+ *                        forward without one); the resolver's buffer is freed stream-ordered on the
+ *                        forward's stream.  Every handle must be released exactly once. */
+typedef struct gsr_forward_resolution {
+    int num_rendered;
+    int binning_layout;
+    void *binning;
+    int redone;          /* 1: the speculation failed and the resolver redid the post-scan kernels */
+} gsr_forward_resolution;
+int gsr_forward_async(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
+                      float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, void *stream);
+int gsr_forward_resolve(unsigned long long handle, gsr_forward_resolution *out);
+int gsr_forward_release(unsigned long long handle);
+/* 1: gsr_forward_resolve would return without waiting; 0: not yet; -1: unknown handle. */
+int gsr_forward_query(unsigned long long handle);
+/* Asynchronous forwards since the last gsr_spec_stats reset, and handles not yet released+resolved. */
+int gsr_async_stats(int *calls, int *pending);
 
 /* Backward of gsr_forward given dL/d(color) (3,H,W).  dL_ddepth is accepted and ignored: the
  * reference discards the depth output (train.py:355-361, densify.py:120-126) and its -w-depth

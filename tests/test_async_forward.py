@@ -1,0 +1,198 @@
+"""Asynchronous forward (-m gpu; gsr_forward_async / gsr_forward_resolve / gsr_forward_release, ABI 17).
+
+A forward whose (device, P, W, H) has pair-count history returns as soon as its kernels are queued,
+without reading num_rendered back.  The device checks the speculative BINNING capacity after the tile
+scan; when it fails, the library's resolver thread redoes the post-scan kernels exactly on its own
+stream and the forward's last kernel (k_fwd_gate) holds the caller's stream until then.  Every output
+must be bitwise the exact path's (images, radii, IMAGE arrays, and the backward, which reads BINNING
+through the resolution), whether the speculation stood or was redone, and whatever the host does
+next (an immediate device synchronisation included: the resolver needs nothing from the caller).
+"""
+import gc
+import time
+
+import pytest
+import torch
+
+import splat_scenes as S
+import diff_gaussian_rasterization as dgr
+from diff_gaussian_rasterization import GaussianRasterizer, _C
+
+pytestmark = pytest.mark.gpu
+
+
+def _forward(a, rs, mode):
+    e = torch.empty(0, device=a["means3D"].device)
+    info = {}
+    out = _C.rasterize_gaussians(rs.bg, a["means3D"], a.get("colors_precomp", e), a["opacities"], a["scales"],
+                                 a["rotations"], 1.0, e, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                                 rs.image_height, rs.image_width, a.get("shs", e), rs.sh_degree, rs.campos, False,
+                                 prepare_backward=True, speculate=mode != "exact", info=info,
+                                 nonblocking=mode == "async")
+    return info, out
+
+
+def _backward(a, rs, out, info, dl):
+    e = torch.empty(0, device=a["means3D"].device)
+    K, color, radii, geom, binning, img, depth = out
+    layout, ptr = info["binning_layout"], None
+    if info["pending"] is not None:
+        K, layout, ptr = info["pending"].resolve()
+    return _C.rasterize_gaussians_backward(rs.bg, a["means3D"], radii, a.get("colors_precomp", e), a["scales"],
+                                           a["rotations"], 1.0, e, rs.viewmatrix, rs.projmatrix, rs.tanfovx,
+                                           rs.tanfovy, dl, a.get("shs", e), rs.sh_degree, rs.campos, geom, K,
+                                           binning, img, prepare_backward=True, binning_layout=layout,
+                                           binning_ptr=ptr), K
+
+
+def _run(a, rs, mode, dl, sync_first=False):
+    info, out = _forward(a, rs, mode)
+    if sync_first:  # the host blocks on the device before anything resolves the forward
+        torch.cuda.synchronize()
+    g, K = _backward(a, rs, out, info, dl)
+    torch.cuda.synchronize()
+    P = a["means3D"].shape[0]
+    W, H = rs.image_width, rs.image_height
+    dec = _C.decode_buffers(P, W, H, K, out[3], out[4], out[5], binning_layout=info["binning_layout"])
+    return {"info": info, "K": K, "color": out[1], "depth": out[6], "radii": out[2], "g": g,
+            "image": {k: dec[k].clone() for k in ("ranges", "n_contrib", "pix_end", "tile_maxc", "seg_off")}}
+
+
+def _same(x, y):
+    assert x["K"] == y["K"]
+    for k in ("color", "depth", "radii"):
+        assert torch.equal(x[k], y[k]), k
+    for k, v in x["image"].items():
+        assert torch.equal(v, y["image"][k]), k
+    for p, q in zip(x["g"], y["g"]):
+        assert (p is None and q is None) or torch.equal(p, q)
+
+
+def _cloud(cuda, P=60_000):
+    a = {k: v for k, v in S.activated_inputs(S.synthetic_cloud(P, 0.01, sh_degree=3, seed=21, device=cuda), 3).items()
+         if k != "means2D" and v is not None}
+    a.pop("colors_precomp", None)
+    return a
+
+
+def test_async_forward_stands_and_is_redone_bitwise(cuda):
+    P, W, H = 60_000, 640, 480
+    a = _cloud(cuda, P)
+    dense = dict(a, scales=a["scales"] * 4.0)  # K 111873 -> 256884 (CPU oracle): past the capacity
+    cam = S.render_settings(W, H, S.intrinsics(500.0, W, H), S.look_at(30, 0.2, 9.0), device=cuda, sh_degree=3)
+    dl = S.upstream_grad(H, W, device=cuda)
+    _C.speculation_stats(reset=True)
+    exact_far = _run(a, cam, "exact", dl)
+    exact_near = _run(dense, cam, "exact", dl)
+    _C.speculation_stats(reset=True)
+    _run(a, cam, "exact", dl)                      # history: the sparse cloud
+    info, out = _forward(a, cam, "async")
+    assert out[0] == -1 and info["pending"] is not None and info["speculated"]
+    del info, out
+    stood = _run(a, cam, "async", dl)              # within the capacity: the queued kernels stand
+    assert stood["info"]["pending"].redone is False
+    _same(stood, exact_far)
+    redone = _run(dense, cam, "async", dl)         # capacity exceeded: the resolver redoes it
+    assert redone["info"]["pending"].redone is True
+    _same(redone, exact_near)
+    _C.speculation_stats(reset=True)
+    _run(a, cam, "exact", dl)
+    held = _run(dense, cam, "async", dl, sync_first=True)  # device sync before any resolve call
+    assert held["info"]["pending"].redone is True
+    _same(held, exact_near)
+
+
+def test_async_forward_redo_with_long_lists(cuda):
+    """A failed speculation whose tiles need the host-sized merge sort (> 4096 pairs): the resolver's
+    redo runs the chunk sorts + merge passes with their temporary buffer."""
+    g = torch.Generator().manual_seed(4)
+    P = 12_000
+    m = torch.zeros(P, 3)
+    m[:, 0] = torch.rand(P, generator=g) * 0.02 - 0.01
+    m[:, 1] = torch.rand(P, generator=g) * 0.02 - 0.01
+    m[:, 2] = torch.rand(P, generator=g) * 2 - 1
+    a = {"means3D": m, "colors_precomp": torch.rand(P, 3, generator=g), "opacities": torch.full((P, 1), 0.05),
+         "scales": torch.full((P, 3), 0.004), "rotations": torch.tensor([[1.0, 0, 0, 0]]).repeat(P, 1)}
+    a = {k: v.to(cuda) for k, v in a.items()}
+    rs = S.render_settings(64, 64, S.intrinsics(64.0, 64, 64), S.look_at(0, 0, 4), device=cuda)
+    dl = S.upstream_grad(64, 64, device=cuda)
+    exact = _run(a, rs, "exact", dl)
+    spread = dict(a, means3D=a["means3D"] * torch.tensor([300.0, 300.0, 1.0], device=cuda))
+    _C.speculation_stats(reset=True)
+    _run(spread, rs, "exact", dl)
+    got = _run(a, rs, "async", dl)
+    assert got["info"]["pending"].redone is True
+    _same(got, exact)
+    nxt = _run(a, rs, "async", dl)  # long lists in the history: no capacity, the blocking exact path
+    assert nxt["info"]["pending"] is None
+    _same(nxt, exact)
+
+
+def test_async_forwards_released_unresolved(cuda):
+    """No-grad forwards queued back to back and dropped without a resolve (inference, train.py:778):
+    every image is the exact one, and the library drops every record once it resolved."""
+    P, W, H = 40_000, 320, 240
+    a = _cloud(cuda, P)
+    cam = S.render_settings(W, H, S.intrinsics(260.0, W, H), S.look_at(10, 0.1, 9.0), device=cuda, sh_degree=3)
+    dense = dict(a, scales=a["scales"] * 3.0)
+    ref = [_forward(x, cam, "exact")[1][1].clone() for x in (a, dense)]
+    _C.speculation_stats(reset=True)
+    _forward(a, cam, "exact")
+    imgs = []
+    for k in range(40):  # the first dense one exceeds the capacity the sparse history gives (redone)
+        x = dense if k % 8 == 5 else a
+        info, out = _forward(x, cam, "async")
+        imgs.append((k % 8 == 5, out[1]))
+        del info, out
+    torch.cuda.synchronize()
+    for dense_k, img in imgs:
+        assert torch.equal(img, ref[1] if dense_k else ref[0])
+    gc.collect()
+    t0 = time.time()
+    while _C.async_stats()[1] and time.time() - t0 < 5:
+        time.sleep(0.01)
+    assert _C.async_stats()[1] == 0
+
+
+@pytest.mark.parametrize("leaf", [True, False])
+def test_autograd_step_async_equals_blocking(cuda, leaf):
+    """The drop-in module's summed multi-view step (train.py:402-418): leaf inputs (deferred multi-view
+    pass, render halves held back while a forward is unresolved) and the reference's non-leaf
+    create_render_arguments inputs (immediate per-view backward) -- images and gradients bitwise those
+    of the blocking forward."""
+    P, W, H = 80_000, 480, 320
+    base = S.synthetic_cloud(P, 0.01, seed=5, device=cuda)
+    cams = [S.render_settings(W, H, S.intrinsics(400.0, W, H), S.look_at(yaw, 0.2, 8.0), device=cuda)
+            for yaw in (0, 40, 80, 120, 160)]
+    dl = S.upstream_grad(H, W, device=cuda)
+
+    def step():
+        params = {k: torch.nn.Parameter(v.clone()) for k, v in base.items()}
+        if leaf:
+            with torch.no_grad():
+                act = S.activated_inputs(params, -1)
+            leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
+        imgs = []
+        for rs in cams:
+            args = dict(leaves, means2D=torch.zeros_like(leaves["means3D"], requires_grad=True)) if leaf \
+                else S.render_arguments(params)
+            imgs.append(GaussianRasterizer(raster_settings=rs)(**args)[0])
+        torch.stack([(i * dl).sum() for i in imgs]).sum().backward()
+        torch.cuda.synchronize()
+        src = leaves if leaf else params
+        return [i.detach() for i in imgs], {k: v.grad for k, v in src.items() if v.grad is not None}
+
+    prev = dgr.set_async_forward(False)
+    try:
+        step()  # history for every view's key
+        ref = step()
+        dgr.set_async_forward(True)
+        got = step()
+        assert _C.async_stats()[0] > 0
+    finally:
+        dgr.set_async_forward(prev)
+    for x, y in zip(ref[0], got[0]):
+        assert torch.equal(x, y)
+    assert ref[1].keys() == got[1].keys()
+    for k in ref[1]:
+        assert torch.equal(ref[1][k], got[1][k]), k

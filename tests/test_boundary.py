@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     L = _C.load_library()
-    assert L.gsr_abi_version() == _C.ABI_VERSION == 16
+    assert L.gsr_abi_version() == _C.ABI_VERSION == 17
     for P in (0, 1, 1000, 1_000_000):
         assert L.gsr_geom_bytes(P) % 256 == 0 and L.gsr_geom_bytes(P) >= 64 * P
     assert L.gsr_image_bytes(1920, 1080, 10) >= 1920 * 1080 * 8
@@ -47,6 +47,20 @@ def test_host_only_entry_points():
     offs = (ctypes.c_size_t * 14)()
     assert L.gsr_buffer_offsets(100, 64, 48, 500, offs, 14) == 14
     assert all(o % 256 == 0 for o in offs)
+
+
+def test_async_forward_handles_host_side():
+    """ABI 17: the asynchronous forward's handle calls validate without a GPU -- an unknown handle is
+    refused by resolve (with a message), reported unknown by query, and ignored by release; no
+    forward has run, so nothing is pending."""
+    L = _C.load_library()
+    r = _C._Resolution()
+    assert L.gsr_forward_resolve(12345, ctypes.byref(r)) == 1
+    assert b"unknown or released forward 12345" in L.gsr_last_error()
+    assert L.gsr_forward_query(12345) == -1
+    assert L.gsr_forward_release(12345) == 0
+    assert _C.async_stats() == (0, 0)
+    assert L.gsr_spec_keys() == 0
 
 
 def test_binning_bytes_follow_segment_length():
