@@ -479,16 +479,116 @@ def _dry_run(args, rank, world):
         dist.destroy_process_group()
 
 
+def step_stats(views_per_step, P, ms):
+    """value / median / quartiles of per-step device intervals (ms list)."""
+    ms = sorted(ms)
+    med = float(np.median(ms))
+    return {"Msplats_per_s": round(views_per_step * P / (med * 1e-3) / 1e6, 2), "median_ms_per_step": round(med, 4),
+            "step_ms_quartiles": [round(float(np.percentile(ms, q)), 4) for q in (25, 50, 75)],
+            "Msplats_per_s_quartiles": [round(views_per_step * P / (float(np.percentile(ms, q)) * 1e-3) / 1e6, 2)
+                                        for q in (75, 50, 25)]}
+
+
+def timed_steps(fn, steps, warmup, dev):
+    """Run fn(it) warmup times, then `steps` times with an event on the current stream after each
+    step: per-step device intervals (ms)."""
+    for it in range(warmup):
+        fn(it)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    ev[0].record(s)
+    for it in range(steps):
+        fn(warmup + it)
+        ev[it + 1].record(s)
+    torch.cuda.synchronize()
+    return [ev[i].elapsed_time(ev[i + 1]) for i in range(steps)]
+
+
+def unchanged_call_site(steps, warmup, cfg, cams, views, dl, dev):
+    """train.py's render step exactly as an unchanged train.py drives it, reported beside ``value``
+    (VERDICT r03 item 1): ONE host thread, torch's current stream, no caller streams; the Gaussian
+    parameters frozen (train.py:155-163 sets requires_grad = False) with the colours train.py renders
+    (colors_precomp, RGB); the step's means and rotations are deep copies, ``.detach()``ed, plus 0.01 x a
+    deformation output (train.py:297-308 -- a (P, 7) leaf stands in for the network, which is out of
+    scope); every view builds its arguments with create_render_arguments (shared.py:29-42: normalize,
+    sigmoid, exp and a fresh ``zeros_like(requires_grad=True) + 0`` means2D) and renders through
+    ``GaussianRasterizer(raster_settings=...)(**args)`` (train.py:359-361); the 5 views' losses are
+    stacked, summed and backpropagated once (train.py:402-418, 767).  The loss of a view is
+    ``(image * dL/dimage).sum()`` with the headline's fixed upstream gradient (the L1 + SSIM and the
+    rigidity loss are out of the metric's scope).  Rasterizer inputs are not leaves, so every view
+    takes the immediate per-view backward; forwards return without a host wait (gsr_forward_async)."""
+    import splat_scenes as S
+    from diff_gaussian_rasterization import GaussianRasterizer
+    P = cfg.P
+    base = S.synthetic_cloud(P, cfg.s0, sh_degree=-1, seed=0, device=dev)  # requires_grad False
+    delta = torch.zeros(P, 7, device=dev, requires_grad=True)
+
+    def one(it):
+        p = {k: v.clone() for k, v in base.items()}  # copy.deepcopy (train.py:297-299)
+        p["means"] = p["means"].detach()
+        p["means"] += delta[:, :3] * 0.01
+        p["rotation_quaternions"] = p["rotation_quaternions"].detach()
+        p["rotation_quaternions"] += delta[:, 3:] * 0.01
+        losses = torch.stack([(GaussianRasterizer(raster_settings=cams[ci])(**S.render_arguments(p))[0] * dl).sum()
+                              for ci in views(it)])
+        losses.sum(dim=0).backward()
+        delta.grad = None  # optimizer.zero_grad()
+
+    ms = timed_steps(one, steps, warmup, dev)
+    out = {"features": "RGB (colors_precomp, as train.py renders)", "views_per_step": len(views(0)),
+           "threads": 1, "streams": "torch's current stream only", "steps": steps,
+           "inputs": "non-leaf (frozen Gaussians, means/rotations = deepcopy.detach() + 0.01 delta, "
+                     "per-view create_render_arguments)",
+           "backward": "one backward of the stacked, summed view losses (immediate per-view rasterizer backward)"}
+    out.update(step_stats(len(views(0)), P, ms))
+    return out
+
+
+def c2_leg(steps, warmup, dev):
+    """BASELINE configs[1] (C2: 100k Gaussians, RGB, the 4 cameras of 800x800 at yaw 0/90/180/270),
+    measured in the default run so the driver records it: one step = the 4 views rendered from one
+    host thread on torch's current stream, their losses summed, one backward into leaf render
+    arguments (deferred multi-view per-Gaussian pass), a fresh zero means2D leaf per render."""
+    import splat_scenes as S
+    import splat_step
+    cfg = S.CONFIGS["C2"]
+    params = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=-1, seed=0, device=dev)
+    with torch.no_grad():
+        act = S.activated_inputs(params, -1)
+    leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
+    cams = S.scene_cameras(cfg, device=dev)
+    dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
+    cur = torch.cuda.current_stream(dev)
+    rstep = splat_step.RenderStep(dev, cams, lambda ci: dict(leaves, means2D=torch.zeros_like(leaves["means3D"],
+                                                                                              requires_grad=True)),
+                                  dl, [cur], threads=False)
+
+    def one(it):
+        rstep(list(range(len(cams))))
+        for v in leaves.values():
+            v.grad = None
+
+    ms = timed_steps(one, steps, warmup, dev)
+    rstep.close()
+    out = {"workload": f"C2: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, 4 cameras per step, fwd+bwd, "
+                       "view losses summed, one backward", "views_per_step": len(cams), "steps": steps,
+           "submission": "one host thread, torch's current stream"}
+    out.update(step_stats(len(cams), cfg.P, ms))
+    return out
+
+
 def train_call_site(steps, cfg, cams, views, dl, dev, streams, sh):
-    """train.py's render call site driven exactly as an unchanged train.py drives it (outside
-    ``value``): the Gaussian parameters are frozen (train.py:155-163 loads them with requires_grad =
+    """train.py's render call site with the benchmark's streams (outside ``value``): the Gaussian
+    parameters are frozen (train.py:155-163 loads them with requires_grad =
     False); the means and rotations of the step are ``p.detach()`` copies plus 0.01 x a deformation
     output (train.py:297-308; here a (P, 7) leaf stands in for the network, which is out of scope);
     every view builds its arguments with create_render_arguments (shared.py:29-42: normalize / sigmoid
     / exp and a fresh ``zeros_like(requires_grad=True) + 0`` means2D); the view losses are summed and
     backpropagated once (train.py:402-418, 767).  The rasterizer's inputs are therefore NOT leaves and
-    every view takes the immediate per-view backward (no deferred multi-view pass).  Same streams and
-    per-stream submitting threads as the headline.  ``sh``: False = the reference's colors_precomp (RGB,
+    every view takes the immediate per-view backward (no deferred multi-view pass).  Unlike an
+    unchanged train.py (``unchanged_call_site``), the views run on the headline's caller-owned streams
+    with one submitting thread per stream.  ``sh``: False = the reference's colors_precomp (RGB,
     what train.py renders), True = SH3 coefficients passed as ``shs`` (the headline's features)."""
     import splat_scenes as S
     import splat_step
@@ -605,6 +705,12 @@ def main():
                     help="steps timed for each call-site variant (0 = skip; N = 1, C3 only)")
     ap.add_argument("--train-steps", type=int, default=10,
                     help="steps timed for the train.py call-site legs (0 = skip; N = 1, C3 only)")
+    ap.add_argument("--unchanged-steps", type=int, default=30,
+                    help="steps timed for the unchanged train.py call site (one thread, current stream, "
+                         "non-leaf inputs, RGB; 0 = skip; N = 1, C3 only)")
+    ap.add_argument("--c2-steps", type=int, default=60,
+                    help="steps timed for the C2 leg (BASELINE configs[1], 4 x 800x800, 100k; 0 = skip; "
+                         "N = 1, C3 only)")
     ap.add_argument("--loss-steps", type=int, default=10,
                     help="steps timed for the L1+SSIM loss legs at the bench resolution (0 = skip; N = 1, C3)")
     ap.add_argument("--densify-steps", type=int, default=5,
@@ -649,7 +755,9 @@ def main():
 
     dist = None
     local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several gloo ranks on one GPU
-    if world > 1:
+    # under a launcher (torch.distributed.run sets WORLD_SIZE) the process group is formed even for one
+    # rank, so `torchrun --nproc-per-node 1 bench.py --backend nccl` runs the RCCL path on one GPU
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         if args.backend == "nccl":
@@ -874,6 +982,11 @@ def main():
                      "fused_activations_ms_per_view": round(fused_ms / per_view, 4),
                      "steps": args.call_site_steps}
     host = {ph: _C.profile_read(ph) for ph in ("host_forward", "host_wait_K", "host_backward")}
+    unchanged = c2 = None
+    if legs and args.unchanged_steps > 0:
+        unchanged = unchanged_call_site(args.unchanged_steps, 5, cfg, cams, views_of, dl, dev)
+    if legs and args.c2_steps > 0:
+        c2 = c2_leg(args.c2_steps, 10, dev)
     train_site = None
     if legs and args.train_steps > 0:
         train_site = {k: train_call_site(args.train_steps, cfg, cams, views_of, dl, dev, streams, sh)
@@ -995,7 +1108,7 @@ def main():
                        "submission": "one host thread per stream" if rstep.pool is not None else "one host thread",
                        "means2D": None if c5_cfg else ("one fresh zero leaf per render (shared.py:38-41)"
                                                        if args.means2d == "per-view" else "one leaf shared by the step's views"),
-                       "backend": args.backend if world > 1 else None},
+                       "backend": args.backend if dist is not None else None},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
@@ -1021,6 +1134,8 @@ def main():
             if solo else None,
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
+            "unchanged_call_site": unchanged,
+            "c2": c2,
             "train_call_site": train_site,
             "call_site": call_site,
             "loss_call_site": loss_site,

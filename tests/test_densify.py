@@ -198,6 +198,65 @@ def test_gpu_densify_large_random_vs_oracle(cuda):
 
 
 @pytest.mark.gpu
+def test_gpu_densify_c3_size_vs_oracle(cuda):
+    """BASELINE configs[2]'s densify.py clone / split at its size: the bench's 1M-Gaussian densify
+    event (bench.py densify_call_site: densify.py's parameter dict, statistics scaled so ~20 % of the
+    seen Gaussians pass the 0.0002 threshold, scene radius at 100 x the median maximum scale, i = 600)
+    through the native path against the golden-pinned numpy restatement of external.py:211-314
+    (oracle/densify_oracle.py) with the split samples shared: row counts bit-exact, every row and
+    Adam moment bit-exact except the split copies' means / log-scales (<= 4e-6 absolute)."""
+    import splat_densify
+    import splat_scenes as S
+    P, it = 1_000_000, 600
+    base = S.synthetic_cloud(P, 0.005, seed=0, device="cpu")
+    rng = np.random.default_rng(7)
+    g = {"means": base["means"].numpy(), "colors": base["colors"].numpy(),
+         "segmentation_masks": np.repeat((rng.random((P, 1)) > 0.5).astype(np.float32), 3, 1),
+         "rotation_quaternions": base["rotation_quaternions"].numpy(),
+         "opacity_logits": base["opacity_logits"].numpy(), "log_scales": base["log_scales"].numpy(),
+         "camera_matrices": np.zeros((50, 3), np.float32), "camera_center": np.zeros((50, 3), np.float32)}
+    keys = list(g)
+    m = {k: (rng.standard_normal(g[k].shape) * 1e-3).astype(np.float32) for k in keys if k not in DO.GAUSSIAN_EXCLUDED}
+    v = {k: (rng.random(g[k].shape) * 1e-6).astype(np.float32) for k in m}
+    cnt = rng.integers(0, 6, P).astype(np.float32)
+    avg = rng.random(P).astype(np.float32) * np.float32(2.5e-4)  # ~20 % of the seen rows >= 0.0002
+    acc = (avg * cnt).astype(np.float32)
+    vis = rng.random(P) > 0.4
+    m2g = (3e-4 * rng.standard_normal((P, 3))).astype(np.float32)
+    mr = rng.integers(0, 9, P).astype(np.float32)
+    sr = float(100.0 * np.median(np.exp(g["log_scales"]).max(axis=1)))
+    params, opt = _gpu_setup(cuda, keys, g, m, v)
+    dv = _dv(cuda, acc, cnt, mr, vis, m2g)
+    drawn = {}
+
+    def sample_fn(mean, std):
+        drawn["s"] = torch.normal(mean=mean, std=std)
+        return drawn["s"]
+
+    info = splat_densify.densify_gaussians(params, dv, sr, opt, it, sample_fn=sample_fn)
+    torch.cuda.synchronize()
+    p2, m2, v2, acc2, cnt2, mr2, oinfo = DO.densify(g, m, v, acc, cnt, mr, vis, m2g, sr, it, drawn["s"].cpu().numpy())
+    assert info["n_split"] > 10_000 and info["n_keep_clone"] > 10_000
+    assert info["n_split"] == oinfo["n_split"] and oinfo["n_clone"] >= info["n_keep_clone"]
+    assert info["P_out"] == p2["means"].shape[0] > P
+    n_base = info["n_keep_orig"] + info["n_keep_clone"]
+    for k in keys:
+        got, ref = params[k].detach().cpu().numpy(), p2[k]
+        assert got.shape == ref.shape, k
+        if k in ("means", "log_scales"):
+            np.testing.assert_array_equal(got[:n_base], ref[:n_base], err_msg=k)
+            np.testing.assert_allclose(got[n_base:], ref[n_base:], rtol=0, atol=4e-6, err_msg=k)
+        else:
+            np.testing.assert_array_equal(got, ref, err_msg=k)
+        if k in m2:
+            np.testing.assert_array_equal(opt.state[params[k]]["exp_avg"].cpu().numpy(), m2[k])
+            np.testing.assert_array_equal(opt.state[params[k]]["exp_avg_sq"].cpu().numpy(), v2[k])
+    np.testing.assert_array_equal(dv.visibility_count.cpu().numpy(), cnt2)
+    np.testing.assert_array_equal(dv.mean_2d_gradients_accumulated.cpu().numpy(), acc2)
+    np.testing.assert_array_equal(dv.max_2d_radii.cpu().numpy(), mr2)
+
+
+@pytest.mark.gpu
 def test_gpu_statistics_match_reference(cuda):
     import splat_densify
     radii, grads = GOLD["dstat_in_radii"], GOLD["dstat_in_grad"]

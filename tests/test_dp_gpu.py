@@ -35,7 +35,36 @@ def test_two_rank_c4_step_equals_single_process(cuda, tmp_path):
     assert b[0]["world"] == 2 and b[1]["world"] == 2
     assert sorted(b[0]["views"] + b[1]["views"]) == list(range(27))
     assert torch.equal(b[0]["bucket"], b[1]["bucket"]), "the ranks hold different reduced gradients"
+    _equals_single_process_c4(cuda, b[0])
 
+
+def test_rccl_one_rank_c4_step(cuda, tmp_path):
+    """The RCCL code path itself on one GPU: `torch.distributed.run --nproc-per-node 1 bench.py --backend
+    nccl` forms a one-rank NCCL (= RCCL) process group (init_process_group("nccl", device_id=...)), the
+    flat gradient bucket is all-reduced in place over RCCL every step with the gsr_grad_fence ordering
+    the next step's gradient writes behind it, and the reduced bucket of the checksum step equals the
+    single-process sum of the 27 rig views."""
+    import json
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    path = str(tmp_path / "c4_rccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(REPO, "bench.py"), "--gpus", "1",
+           "--backend", "nccl", "--config", "C4", "--steps", "2", "--warmup", "1", "--probe-steps", "0",
+           "--no-cpu-baseline", "--grad-checksum", path]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["config"]["backend"] == "nccl", line["config"]
+    b = torch.load(f"{path}.rank0.pt", weights_only=True)
+    assert b["world"] == 1 and sorted(b["views"]) == list(range(27))
+    _equals_single_process_c4(cuda, b)
+
+
+def _equals_single_process_c4(cuda, b):
+    """The reduced bucket `b` against one process rendering all 27 C4 views summed."""
     # single process: the same leaves (bench.py's C4 setup), all 27 views summed, one backward
     cfg = S.CONFIGS["C4"]
     p = S.synthetic_cloud(cfg.P, cfg.s0, sh_degree=-1, seed=0, device=cuda)
@@ -53,9 +82,9 @@ def test_two_rank_c4_step_equals_single_process(cuda, tmp_path):
     finally:
         step.close()
     torch.cuda.synchronize()
-    names = b[0]["names"]
+    names = b["names"]
     assert names == [k for k in leaves if k != "means2D"]
-    got = b[0]["bucket"].numpy().astype(np.float64)
+    got = b["bucket"].numpy().astype(np.float64)
     o = 0
     for k in names:
         ref = leaves[k].grad.detach().cpu().numpy().reshape(-1).astype(np.float64)
