@@ -8,6 +8,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <chrono>
@@ -344,11 +345,83 @@ void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
     if (outcome < 0) ++g_spec_misses;
 }
 
+// ---- the backward's item list on an auxiliary stream (ABI 17) ---------------------------------
+// k_bwd_items is one 1024-thread block (~30 us alone) that only the backward reads.  On the caller's
+// stream it sits between the forward's render and whatever the caller queues next (train.py: the
+// view's loss, the next view's activations and forward), with the rest of the chip idle.  The forward
+// therefore queues it on a per-device library stream, forked from the caller's stream by an event
+// after the render; the backward's render half waits for it (items_join) before k_render_bwd.  The
+// caller keeps the BINNING buffer from being reused before the auxiliary stream is done with it
+// (gsr_forward_info.aux_stream: torch's record_stream on an ExternalStream of it).
+bool g_items_aux = [] {
+    const char *e = getenv("GSR_ITEMS_AUX");
+    return !(e && e[0] == '0');
+}();
+std::mutex g_items_mu;
+std::map<int, hipStream_t> g_aux;                       // device -> auxiliary stream
+std::unordered_map<const void *, hipEvent_t> g_items;  // item list -> event after its k_bwd_items
+std::vector<hipEvent_t> g_items_evpool;
+
+hipEvent_t items_event() {  // (g_items_mu held)
+    if (!g_items_evpool.empty()) { hipEvent_t e = g_items_evpool.back(); g_items_evpool.pop_back(); return e; }
+    hipEvent_t e = nullptr;
+    return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? e : nullptr;
+}
+
+hipStream_t aux_stream(int dev) {  // (g_items_mu held)
+    hipStream_t &a = g_aux[dev];
+    if (!a && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) a = nullptr;
+    return a;
+}
+
+// Queue the item list of `items` (launch(stream)) on the auxiliary stream after the work queued so far on
+// `s`; returns the auxiliary stream, or nullptr when it ran on `s` itself.
+template <typename Launch>
+hipError_t items_fork(int dev, hipStream_t s, const void *items, Launch launch, hipStream_t *used) {
+    *used = nullptr;
+    std::lock_guard<std::mutex> lk(g_items_mu);
+    hipStream_t aux = g_items_aux ? aux_stream(dev) : nullptr;
+    hipEvent_t fork = aux ? items_event() : nullptr, join = aux ? items_event() : nullptr;
+    if (!aux || !fork || !join) {
+        if (fork) g_items_evpool.push_back(fork);
+        if (join) g_items_evpool.push_back(join);
+        return launch(s);
+    }
+    hipError_t r = hipEventRecord(fork, s);
+    if (r == hipSuccess) r = hipStreamWaitEvent(aux, fork, 0);
+    if (r == hipSuccess) r = launch(aux);
+    if (r == hipSuccess) r = hipEventRecord(join, aux);
+    g_items_evpool.push_back(fork);  // a pending record may be re-recorded: the wait above is queued
+    if (r != hipSuccess) { g_items_evpool.push_back(join); return r; }
+    auto it = g_items.find(items);
+    if (it != g_items.end()) g_items_evpool.push_back(it->second);
+    g_items[items] = join;
+    if (g_items.size() > 256) {  // forwards whose backward never came: drop finished entries
+        for (auto e = g_items.begin(); e != g_items.end();)
+            if (hipEventQuery(e->second) == hipSuccess) { g_items_evpool.push_back(e->second); e = g_items.erase(e); }
+            else ++e;
+    }
+    *used = aux;
+    return hipSuccess;
+}
+
+// The backward's stream waits for the item list at `items` when the forward built it on the
+// auxiliary stream.
+hipError_t items_join(const void *items, hipStream_t s) {
+    std::lock_guard<std::mutex> lk(g_items_mu);
+    auto it = g_items.find(items);
+    if (it == g_items.end()) return hipSuccess;
+    const hipError_t r = hipStreamWaitEvent(s, it->second, 0);
+    g_items_evpool.push_back(it->second);
+    g_items.erase(it);
+    return r;
+}
+
 // ---- asynchronous forwards (ABI 17, gsr_forward_async) ------------------------------------------
 // A speculative forward whose capacity came from the key's history returns as soon as its kernels are
 // queued, without reading num_rendered back.  Each such forward takes a slot of a host-mapped ring:
-// k_bin_scan publishes K and the list-class counts into the slot's words, and the last kernel of the
-// forward, k_fwd_gate, holds the caller's stream only when the device found the capacity too small.
+// k_bin_scan publishes K and the list-class counts into the slot's words, and the speculative
+// k_render_fwd holds the caller's stream (gate_wait) only when the device found the capacity too small.
 // The resolver thread (one per process, no Python, no caller locks) reads every pending slot; on a
 // failed speculation it redoes the post-scan kernels exactly on its own stream, into a BINNING buffer
 // it allocates stream-ordered (hipMallocAsync), and then opens the gate.  Outputs are therefore the
@@ -590,6 +663,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     info->binning_layout = 0;
     info->speculated = 0;
     info->pending = 0;
+    info->aux_stream = nullptr;
     if (a.P == 0) {  // reference: colour/depth stay zero (no background) when there are no Gaussians
         HIP_TRY(launch_zero(out_color, 3 * npix, s));
         HIP_TRY(launch_zero(out_depth, npix, s));
@@ -613,6 +687,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
             if (slot >= 0) {
                 af = std::make_shared<AsyncFwd>();
                 af->slot = slot;
+                af->seq = ++g_as_seq;
                 words_h = slot_h(slot);
                 words_d = slot_d(slot);
             }
@@ -649,24 +724,31 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         FwdArgs sa = a;
         carve_binning(sa, spec_bin, (int)cap);
         sa.spec_ok = sa.meta + 1;
+        if (af) {  // a failed speculation holds the stream in the speculative render until it is redone
+            sa.gate = words_d + kGateWord;
+            sa.gate_seq = af->seq;
+            sa.gate_err = gate_err_d();
+        }
         { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(sa, 0, s)); }
         { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(sa, 0, 0, 0, nullptr, s)); }
         { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(sa, s)); }
         if (GSR_FWD_ITEMS && g->prepare_backward) {
-            Phase ph(s, "bwd_items");
-            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc,
-                                         (uint2 *)(spec_bin + BinningLayout((int)cap, a.P).total), s, sa.spec_ok));
+            uint2 *items = (uint2 *)(spec_bin + BinningLayout((int)cap, a.P).total);
+            hipStream_t used = nullptr;
+            HIP_TRY(items_fork(dev, s, items, [&](hipStream_t q) {
+                Phase ph(q, "bwd_items");
+                return launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, q, sa.spec_ok);
+            }, &used));
+            info->aux_stream = used;
         }
     }
     if (af) {  // asynchronous: gate the stream on the verdict and return
         std::lock_guard<std::mutex> lk(g_as_mu);
         af->id = g_as_next_id++;
-        af->seq = ++g_as_seq;
         af->dev = dev; af->s = s; af->cap = cap; af->T = T; af->key = key;
         af->prep = g->prepare_backward != 0;
         af->a = a;
         af->spec_bin = spec_bin;
-        HIP_TRY(launch_fwd_gate(a.meta + 1, words_d + kGateWord, af->seq, gate_err_d(), s));
         g_as[af->id] = af;
         info->num_rendered = -1;
         info->binning_layout = (int)cap;
@@ -725,8 +807,13 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)(bin + bin_bytes + item_bytes), s)); }
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // the backward's item list, built here, off its critical path
-        Phase ph(s, "bwd_items");
-        HIP_TRY(launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, (uint2 *)(bin + bin_bytes), s));
+        uint2 *items = (uint2 *)(bin + bin_bytes);
+        hipStream_t used = nullptr;
+        HIP_TRY(items_fork(dev, s, items, [&](hipStream_t q) {
+            Phase ph(q, "bwd_items");
+            return launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, q);
+        }, &used));
+        if (used) info->aux_stream = used;
     }
     info->binning_layout = (int)K;
     spec_record(key, K, n_vlong > 0, cap ? -1 : 0);
@@ -895,6 +982,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // built by the forward, after the binning arrays
         a.items = (uint2 *)((char *)binning + BinningLayout(layout, a.P).total);
+        HIP_TRY(items_join(a.items, s));  // (queued on the auxiliary stream)
     } else {
         a.items = (uint2 *)(scr + SL.items);
         Phase ph(s, "bwd_items");

@@ -680,6 +680,25 @@ __global__ __launch_bounds__(512) void k_merge_pass(int T, const uint32_t *__res
 #ifndef GSR_FWD_Q8
 #define GSR_FWD_Q8 1  // 8x8 quarters per wave (0: 16x4 strips, the backward's quarters)
 #endif
+// Asynchronous forwards (gsr_forward_async): when k_bin_scan found the speculative capacity too
+// small (spec_ok == 0: the queued kernels return at once), the speculative k_render_fwd's first wave
+// holds the stream until the library's resolver thread has redone the post-scan kernels exactly on its
+// own stream and published `seq` in the forward's gate word (host-mapped) -- everything the caller
+// queues after the forward is ordered behind it.  When the speculation stood nothing waits.  A gate that
+// never opens (the resolver died) is abandoned after kGateTimeoutTicks with an error word set, so a
+// failure cannot hang the device.
+constexpr uint64_t kGateTimeoutTicks = 2000000000ull;  // s_memrealtime runs at 100 MHz: 20 s
+__device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *err) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
+        __builtin_amdgcn_s_sleep(100);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+            if (threadIdx.x == 0) __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_render_fwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
     const uint4 *__restrict__ pairs,
@@ -687,7 +706,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
     float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok,
-    int ks) {
+    int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err) {
     __shared__ uint64_t s_key[kFwdSortCap];
     __shared__ union {
         uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
@@ -700,7 +719,10 @@ __global__ __launch_bounds__(256) void k_render_fwd(
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
+    if (spec_ok && *spec_ok == 0u) {  // speculative launch whose capacity failed: redone by the host
+        if (gate && blockIdx.x == 0 && threadIdx.x < 64) gate_wait(gate, gate_seq, gate_err);  // (asynchronous)
+        return;
+    }
     const int tile = (int)tile_order[blockIdx.x];
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -869,27 +891,6 @@ __global__ __launch_bounds__(256) void k_render_fwd(
 #endif
 }
 
-// The end of an asynchronous forward (gsr_forward_async): when k_bin_scan found the speculative
-// capacity too small (spec_ok == 0: the queued kernels returned at once), hold this stream until the
-// library's resolver thread has redone the post-scan kernels exactly on its own stream and published
-// `seq` in the slot's gate word (host-mapped).  Everything the caller queues after the forward is
-// ordered behind this one-wave kernel; when the speculation stood it returns at once.  A gate that
-// never opens (the resolver died) is abandoned after kGateTimeoutTicks with an error word set, so a
-// failure cannot hang the device.
-constexpr uint64_t kGateTimeoutTicks = 2000000000ull;  // s_memrealtime runs at 100 MHz: 20 s
-__global__ __launch_bounds__(64) void k_fwd_gate(const uint32_t *__restrict__ spec_ok, const uint32_t *gate,
-                                                 uint32_t seq, uint32_t *err) {
-    if (*spec_ok) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while ((int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
-        __builtin_amdgcn_s_sleep(100);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
-            if (threadIdx.x == 0) __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
-        }
-    }
-}
-
 __global__ void k_zero_f32(float *p, size_t n) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = 0.f;
@@ -996,12 +997,8 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                                    a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
-                                   a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P));
-    return hipGetLastError();
-}
-
-hipError_t launch_fwd_gate(const uint32_t *spec_ok, const uint32_t *gate, uint32_t seq, uint32_t *err, hipStream_t s) {
-    k_fwd_gate<<<1, 64, 0, s>>>(spec_ok, gate, seq, err);
+                                   a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
+                                   a.gate_err);
     return hipGetLastError();
 }
 

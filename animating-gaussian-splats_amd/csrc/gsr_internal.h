@@ -26,6 +26,9 @@ struct FwdArgs {
     // were queued with before the host read K (0: exact path), and the device flag they check
     // (meta + 1, written by k_bin_scan; nullptr: exact path)
     uint32_t spec_cap; const uint32_t *spec_ok;
+    // asynchronous forward (gsr_forward_async): the gate word the speculative render's first wave waits
+    // on when the speculation failed, the value that opens it, and the timeout error word
+    const uint32_t *gate; uint32_t gate_seq; uint32_t *gate_err;
 };
 // blocks of the speculative k_tile_sort launch (they loop over the device-side list count)
 constexpr int kSpecSortBlocks = 512;
@@ -61,8 +64,6 @@ hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, 
                             hipStream_t s);
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s);
 hipError_t launch_zero(float *p, size_t n, hipStream_t s);
-// asynchronous forward: holds the stream until a failed speculation has been redone (gsr_api.hip)
-hipError_t launch_fwd_gate(const uint32_t *spec_ok, const uint32_t *gate, uint32_t seq, uint32_t *err, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmatrix, uint8_t *present,
                                hipStream_t s);
 

@@ -64,7 +64,7 @@ class _Gaussians(ctypes.Structure):
 
 class _ForwardInfo(ctypes.Structure):  # gsr_forward_info (ABI 17)
     _fields_ = [("num_rendered", ctypes.c_int), ("binning_layout", ctypes.c_int), ("speculated", ctypes.c_int),
-                ("pending", ctypes.c_ulonglong)]
+                ("pending", ctypes.c_ulonglong), ("aux_stream", ctypes.c_void_p)]
 
 
 class _Resolution(ctypes.Structure):  # gsr_forward_resolution (ABI 17)
@@ -420,11 +420,25 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                                                color.data_ptr(), depth.data_ptr(), radii.data_ptr() if P else None,
                                                int(bool(speculate)), ctypes.byref(fi), _stream_ptr(dev)))
     pending = AsyncForward(fi.pending) if fi.pending else None
+    b = alloc.buffers
+    if fi.aux_stream and GSR_BUF_BINNING in b:  # the item list is written on the library's auxiliary
+        b[GSR_BUF_BINNING].record_stream(_external_stream(fi.aux_stream, dev))  # stream: no early reuse
     if info is not None:
         info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated),
                     pending=pending)
-    b = alloc.buffers
     return fi.num_rendered, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
+
+
+_EXT_STREAMS = {}
+
+
+def _external_stream(ptr, dev):
+    """torch's handle of a library stream (cached per device and stream)."""
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), int(ptr))
+    st = _EXT_STREAMS.get(key)
+    if st is None:
+        st = _EXT_STREAMS[key] = torch.cuda.ExternalStream(int(ptr), device=torch.device("cuda", key[0]))
+    return st
 
 
 def speculation_stats(reset=False):
