@@ -343,8 +343,173 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
-    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales,
-                                     rotations, cov3Ds_precomp, raster_settings, torch.is_grad_enabled())
+    args = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
+    bridged = _bridged_inputs(args)
+    if bridged:
+        return _on_view_stream(args, bridged, raster_settings)
+    return _RasterizeGaussians.apply(*args, raster_settings, torch.is_grad_enabled())
+
+
+# ---- library view streams for non-leaf inputs (the unchanged train.py / densify.py call shape) ------
+# train.py renders its 5 views from one thread on torch's current stream C with NON-leaf inputs
+# (create_render_arguments: normalize / sigmoid / exp / zeros + 0, shared.py:29-42) and one backward of
+# the summed losses (train.py:402-418).  Every gradient the rasterizer returns then goes to a node of the
+# caller's graph that ran on C, and the autograd engine makes C wait for the producing stream the moment
+# it hands a gradient over (InputBuffer::add).  It hands them over right after each view's backward node
+# returns, and it runs the nodes by descending sequence number: view k's consumers (its normalize etc.)
+# come before view k-1's loss backward.  So the views' backward kernels would run strictly one after
+# another, whatever stream they were queued on.
+# Here each such view runs on one of the library's view streams L (round robin): L waits for C, the
+# forward is queued on L, C waits for L before the outputs are used (the forward stays ordered as the
+# caller wrote it).  The non-leaf inputs go through a _StreamBridge node created by a helper thread --
+# sequence numbers are per thread, so the bridge has the lowest priority of the pass: the engine runs
+# every view's loss backward and rasterizer backward (queued on that view's L, so they overlap on the
+# GPU) before any bridge, and each bridge then hands its view's gradients to C (record_stream + wait).
+# Leaf inputs are not bridged (the backward adds into their .grad in place on L); the end of the pass
+# makes C wait for every L used.  Results are bitwise those of one stream: every gradient write is
+# ordered (gsr_grad_fence / ordered_grad_write) and each consumer waits for its producer.
+_VIEW_STREAMS = {"on": os.environ.get("GSR_VIEW_STREAMS", "1") != "0", "n": 3, "pool": {}, "next": {}}
+
+
+def set_view_streams(on: bool) -> bool:
+    """Enable / disable the library view streams for non-leaf inputs; returns the previous setting."""
+    prev = _VIEW_STREAMS["on"]
+    _VIEW_STREAMS["on"] = bool(on)
+    return prev
+
+
+def _bridged_inputs(args):
+    """Indices of the inputs a view-stream render bridges (non-leaf, requiring grad), or () when the
+    call takes the caller's stream (disabled, no grad, no such input, CPU tensors)."""
+    if not _VIEW_STREAMS["on"] or not torch.is_grad_enabled() or not args[0].is_cuda:
+        return ()
+    return tuple(i for i, t in enumerate(args)
+                 if isinstance(t, torch.Tensor) and t.numel() and t.requires_grad and not t.is_leaf)
+
+
+def _view_stream(dev):
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    pool = _VIEW_STREAMS["pool"].get(key)
+    if pool is None:
+        pool = _VIEW_STREAMS["pool"][key] = [torch.cuda.Stream(torch.device("cuda", key))
+                                              for _ in range(_VIEW_STREAMS["n"])]
+    k = _VIEW_STREAMS["next"].get(key, 0)
+    _VIEW_STREAMS["next"][key] = (k + 1) % len(pool)
+    return pool[k]
+
+
+class _StreamBridge(torch.autograd.Function):
+    """Identity over a view's non-leaf inputs, created on the view's stream by the helper thread (low
+    sequence number: the engine runs it after every other ready node).  Its backward hands the view's
+    gradients to the caller's stream."""
+
+    @staticmethod
+    def forward(ctx, caller, *xs):
+        ctx.caller = caller
+        return tuple(x.view_as(x) for x in xs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        for g in gs:
+            if g is not None:
+                g.record_stream(ctx.caller)  # produced on this view's stream, consumed on the caller's
+        ctx.caller.wait_stream(torch.cuda.current_stream())
+        return (None,) + gs
+
+
+class _BridgeThread:
+    """The helper thread that creates _StreamBridge nodes (its autograd sequence numbers stay far below
+    the caller's); one synchronous hand-off per view-stream render."""
+
+    def __init__(self):
+        import queue
+        self.q = queue.Queue()
+        self.t = threading.Thread(target=self._run, name="gsr-bridge", daemon=True)
+        self.t.start()
+
+    def _run(self):
+        while True:
+            job, done, box = self.q.get()
+            try:
+                box["out"] = job()
+            except BaseException as e:  # noqa: BLE001 - re-raised in the caller
+                box["err"] = e
+            done.set()
+
+    def call(self, job):
+        done, box = threading.Event(), {}
+        self.q.put((job, done, box))
+        done.wait()
+        if "err" in box:
+            raise box["err"]
+        return box["out"]
+
+
+_bridge_thread = None
+_bridge_lock = threading.Lock()
+_sync_tasks = {}  # graph task -> the (caller stream, view streams) its end-of-pass callback joins
+
+
+def _bridge(xs, caller, L, dev):
+    global _bridge_thread
+    with _bridge_lock:
+        if _bridge_thread is None:
+            _bridge_thread = _BridgeThread()
+
+    def job():
+        with torch.enable_grad(), torch.cuda.device(dev), torch.cuda.stream(L):
+            return _StreamBridge.apply(caller, *xs)
+    out = _bridge_thread.call(job)
+    return out if isinstance(out, tuple) else (out,)
+
+
+def _on_view_stream(args, bridged, rs):
+    dev = args[0].device
+    C = torch.cuda.current_stream(dev)
+    L = _view_stream(dev)
+    L.wait_stream(C)  # the caller's inputs (activations) are ready on L
+    for t in args:
+        if t.numel() and t.is_cuda:
+            t.record_stream(L)  # read on L (forward and backward) -- no early reuse on C
+    xs = list(args)
+    out = _bridge([args[i] for i in bridged], C, L, dev)
+    for i, t in zip(bridged, out):
+        xs[i] = t
+    _view_tls.cur = (C, L)  # read by the Function's forward (same thread, synchronous)
+    try:
+        with torch.cuda.stream(L):
+            color, radii, depth = _RasterizeGaussians.apply(*xs, rs, True)
+    finally:
+        _view_tls.cur = None
+    for t in (color, radii, depth):
+        t.record_stream(C)
+    C.wait_stream(L)  # the outputs are used on the caller's stream
+    return color, radii, depth
+
+
+_view_tls = threading.local()
+
+
+def _view_stream_backward(ctx):
+    """Called from the rasterizer's backward node when its forward ran on a view stream: the backward
+    pass gets one end-of-pass callback that makes the caller's stream wait for every view stream the
+    pass used (leaf gradients are written in place there)."""
+    task = torch._C._current_graph_task_id()
+    if task < 0:
+        return
+    with _bridge_lock:
+        ent = _sync_tasks.get(task)
+        new = ent is None
+        if new:
+            ent = _sync_tasks[task] = (ctx.view_caller, set())
+        ent[1].add(ctx.view_stream)
+    if new:
+        def join():
+            with _bridge_lock:
+                caller, streams = _sync_tasks.pop(task, (None, ()))
+            for st in streams:
+                caller.wait_stream(st)
+        torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
@@ -366,6 +531,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.num_rendered = num_rendered
         ctx.binning_layout = info["binning_layout"]
         ctx.pending = info["pending"]  # an asynchronous forward: resolved by the backward
+        ctx.view_caller, ctx.view_stream = getattr(_view_tls, "cur", None) or (None, None)
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
         ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
         ctx.tensor_pos = _tensor_positions((means3D, means2D, sh, colors_precomp, opacities, scales,
@@ -378,6 +544,8 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, grad_depth):
+        if ctx.view_stream is not None:
+            _view_stream_backward(ctx)
         if grad_out_color is None:  # only depth was used: it carries no gradient (-w-depth)
             return (None,) * 10
         rs = ctx.raster_settings
