@@ -462,7 +462,8 @@ uint32_t *g_slot_h = nullptr, *g_slot_d = nullptr;  // kAsyncSlots * kSlotWords 
 std::vector<uint8_t> g_slot_busy;
 int g_slot_next = 0;
 std::string g_async_err;  // a failed redo or gate, reported by the next call
-bool g_resolver_started = false;
+bool g_resolver_started = false, g_resolver_stop = false;
+std::thread g_resolver;
 
 uint32_t *slot_h(int k) { return g_slot_h + (size_t)k * kSlotWords; }
 uint32_t *slot_d(int k) { return g_slot_d + (size_t)k * kSlotWords; }
@@ -484,8 +485,9 @@ bool async_init() {
         g_slot_h = h; g_slot_d = d;
         g_slot_busy.assign(kAsyncSlots, 0);
     }
-    if (!g_resolver_started) {
-        std::thread(resolver_main).detach();  // lives for the process; holds no caller resources
+    if (!g_resolver_started) {  // lives until gsr_async_shutdown (the binding's atexit hook)
+        g_resolver_stop = false;
+        g_resolver = std::thread(resolver_main);
         g_resolver_started = true;
     }
     return true;
@@ -614,9 +616,11 @@ void resolver_main() {
             g_as_done.notify_all();
             continue;
         }
+        if (g_resolver_stop && !todo) break;
         if (pending) g_as_wake.wait_for(lk, std::chrono::microseconds(50));
         else g_as_wake.wait(lk);
     }
+    for (auto &kv : streams) (void)hipStreamDestroy(kv.second);
 }
 
 }  // namespace
@@ -915,6 +919,20 @@ int gsr_forward_release(unsigned long long handle) {
     const int st = it->second->state;
     if (st == 1 || st == 3 || st == -1) async_reap(it);
     else g_as_wake.notify_one();  // reaped by the resolver once resolved
+    return GSR_OK;
+}
+
+int gsr_async_shutdown(void) {
+    std::thread t;
+    {
+        std::lock_guard<std::mutex> lk(g_as_mu);
+        if (!g_resolver_started) return GSR_OK;
+        g_resolver_stop = true;
+        g_resolver_started = false;
+        t = std::move(g_resolver);
+    }
+    g_as_wake.notify_all();
+    if (t.joinable()) t.join();
     return GSR_OK;
 }
 

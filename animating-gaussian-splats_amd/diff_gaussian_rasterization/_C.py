@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
     "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes", "gsr_prealloc_alloc", "gsr_spec_binning_bytes",
     "gsr_forward_async", "gsr_forward_resolve", "gsr_forward_release", "gsr_forward_query", "gsr_async_stats",
-    "gsr_spec_keys",
+    "gsr_spec_keys", "gsr_async_shutdown",
 )
 
 
@@ -128,6 +128,10 @@ def load_library():
     L.gsr_forward_query.argtypes = [ctypes.c_ulonglong]
     L.gsr_async_stats.restype = i
     L.gsr_async_stats.argtypes = [ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.gsr_async_shutdown.restype = i
+    L.gsr_async_shutdown.argtypes = []
+    import atexit
+    atexit.register(L.gsr_async_shutdown)  # the resolver thread stops before the HIP runtime goes
     L.gsr_backward.restype = i
     L.gsr_backward.argtypes = [ctypes.POINTER(_Camera), ctypes.POINTER(_Gaussians), vp, i, vp, vp, vp,
                                vp, vp, _ALLOC_FN, vp, ctypes.POINTER(_Grads), vp]

@@ -545,11 +545,12 @@ def unchanged_call_site(steps, warmup, cfg, cams, views, dl, dev):
     return out
 
 
-def c2_leg(steps, warmup, dev):
+def c2_leg(steps, warmup, dev, nstreams=3):
     """BASELINE configs[1] (C2: 100k Gaussians, RGB, the 4 cameras of 800x800 at yaw 0/90/180/270),
-    measured in the default run so the driver records it: one step = the 4 views rendered from one
-    host thread on torch's current stream, their losses summed, one backward into leaf render
-    arguments (deferred multi-view per-Gaussian pass), a fresh zero means2D leaf per render."""
+    measured in the default run so the driver records it: one step = the 4 views rendered from ONE
+    host thread over `nstreams` streams (the forwards do not wait for their pair counts, so one thread
+    keeps every stream fed), their losses summed, one backward into leaf render arguments (deferred
+    multi-view per-Gaussian pass), a fresh zero means2D leaf per render."""
     import splat_scenes as S
     import splat_step
     cfg = S.CONFIGS["C2"]
@@ -560,12 +561,17 @@ def c2_leg(steps, warmup, dev):
     cams = S.scene_cameras(cfg, device=dev)
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
     cur = torch.cuda.current_stream(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
+    for st in streams:
+        st.wait_stream(cur)
     rstep = splat_step.RenderStep(dev, cams, lambda ci: dict(leaves, means2D=torch.zeros_like(leaves["means3D"],
                                                                                               requires_grad=True)),
-                                  dl, [cur], threads=False)
+                                  dl, streams, threads=False)
 
     def one(it):
         rstep(list(range(len(cams))))
+        for st in streams:
+            cur.wait_stream(st)  # the step ends on the current stream (its timing event)
         for v in leaves.values():
             v.grad = None
 
@@ -573,7 +579,7 @@ def c2_leg(steps, warmup, dev):
     rstep.close()
     out = {"workload": f"C2: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, 4 cameras per step, fwd+bwd, "
                        "view losses summed, one backward", "views_per_step": len(cams), "steps": steps,
-           "submission": "one host thread, torch's current stream"}
+           "submission": f"one host thread, {nstreams} streams"}
     out.update(step_stats(len(cams), cfg.P, ms))
     return out
 

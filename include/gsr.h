@@ -208,6 +208,9 @@ int gsr_forward_release(unsigned long long handle);
 int gsr_forward_query(unsigned long long handle);
 /* Asynchronous forwards since the last gsr_spec_stats reset, and handles not yet released+resolved. */
 int gsr_async_stats(int *calls, int *pending);
+/* Stops the resolver thread once it has no redo in flight (call at process exit, before the HIP
+ * runtime is torn down; a later asynchronous forward starts it again). */
+int gsr_async_shutdown(void);
 
 /* Backward of gsr_forward given dL/d(color) (3,H,W).  dL_ddepth is accepted and ignored: the
  * reference discards the depth output (train.py:355-361, densify.py:120-126) and its -w-depth
