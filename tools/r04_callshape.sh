@@ -12,6 +12,7 @@ GSR_ITEMS_AUX=0 run python -u tools/callshape_probe.py no_items_aux
 run python -u tools/callshape_probe.py no_async_no_vs --no-async --no-view-streams --profile
 run python -u tools/callshape_probe.py all_on_again
 cat $O
+bash tools/r04_headline_ab.sh || exit $?
 R=$(pwd); T=$R/gpurun_out/r04/trace_unchanged
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$T" -- python3 "$R/tools/callshape_probe.py" traced --steps 20 > "$R/gpurun_out/r04/trace_unchanged.log" 2>&1 || { echo "trace failed"; exit 1; }
