@@ -460,6 +460,7 @@ uint64_t g_as_next_id = 1;
 uint32_t g_as_seq = 0;
 uint32_t *g_slot_h = nullptr, *g_slot_d = nullptr;  // kAsyncSlots * kSlotWords words + 16 (error words)
 std::vector<uint8_t> g_slot_busy;
+std::vector<hipEvent_t> g_as_evpool;  // k_bin_scan events of reaped forwards
 int g_slot_next = 0;
 std::string g_async_err;  // a failed redo or gate, reported by the next call
 bool g_resolver_started = false, g_resolver_stop = false;
@@ -534,7 +535,7 @@ void async_reap(std::unordered_map<uint64_t, std::shared_ptr<AsyncFwd>>::iterato
         if (cur != f.dev) (void)hipSetDevice(cur);
         f.own = nullptr;
     }
-    if (f.ev_scan) (void)hipEventDestroy(f.ev_scan);
+    if (f.ev_scan) g_as_evpool.push_back(f.ev_scan);  // a pending record may be re-recorded later
     f.ev_scan = nullptr;
     if (f.slot >= 0) g_slot_busy[f.slot] = 0;
     g_as.erase(it);
@@ -703,7 +704,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
             if (!*f || (*f)->id) return;
             std::lock_guard<std::mutex> lk(g_as_mu);
             g_slot_busy[(*f)->slot] = 0;
-            if ((*f)->ev_scan) (void)hipEventDestroy((*f)->ev_scan);
+            if ((*f)->ev_scan) g_as_evpool.push_back((*f)->ev_scan);
         }
     } slot_guard{&af};
     if (!af) {
@@ -717,7 +718,11 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     { Phase ph(s, "bin_count"); HIP_TRY(launch_bin_count(a, s)); }
     { Phase ph(s, "bin_scan"); HIP_TRY(launch_bin_scan(a, words_d, s)); }
     if (af) {
-        HIP_TRY(hipEventCreateWithFlags(&af->ev_scan, hipEventDisableTiming));
+        {
+            std::lock_guard<std::mutex> lk(g_as_mu);
+            if (!g_as_evpool.empty()) { af->ev_scan = g_as_evpool.back(); g_as_evpool.pop_back(); }
+        }
+        if (!af->ev_scan) HIP_TRY(hipEventCreateWithFlags(&af->ev_scan, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(af->ev_scan, s));
     }
     const size_t spec_item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;
