@@ -473,6 +473,23 @@ uint32_t *gate_err_d() { return g_slot_d + (size_t)kAsyncSlots * kSlotWords; }
 
 void resolver_main();
 
+// The resolver's stream of each device.  A failed speculation holds the forward's stream in a
+// spinning wave until the redo on this stream is done, so this stream must never sit behind that wave
+// in a shared hardware queue (a process's streams share GPU_MAX_HW_QUEUES queues per priority): a
+// stream with a CU mask always gets a queue of its own (the mask enables every CU).  Created on the
+// caller's thread at the first asynchronous forward of the device (g_as_mu held).
+std::map<int, hipStream_t> g_resolver_streams;
+hipStream_t resolver_stream(int dev) {
+    hipStream_t &h = g_resolver_streams[dev];
+    if (h) return h;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+    if (hipExtStreamCreateWithCUMask(&h, (uint32_t)mask.size(), mask.data()) != hipSuccess) h = nullptr;
+    return h;
+}
+
 // (g_as_mu held) the slot ring and the resolver thread, on first use
 bool async_init() {
     if (!g_slot_h) {
@@ -543,10 +560,9 @@ void async_reap(std::unordered_map<uint64_t, std::shared_ptr<AsyncFwd>>::iterato
 
 // The exact post-scan kernels of a failed speculation, on the resolver's stream of the forward's
 // device, then the gate opens.  Runs without g_as_mu.
-int async_redo(AsyncFwd &f, std::map<int, hipStream_t> &streams) {
+int async_redo(AsyncFwd &f, hipStream_t H) {
     (void)hipSetDevice(f.dev);
-    hipStream_t &H = streams[f.dev];
-    if (!H) HIP_TRY(hipStreamCreateWithFlags(&H, hipStreamNonBlocking));
+    if (!H) return fail(GSR_ERR_HIP, "asynchronous forward: no resolver stream on device %d", f.dev);
     HIP_TRY(hipStreamWaitEvent(H, f.ev_scan, 0));
     const uint32_t *w = slot_h(f.slot);
     const uint32_t K = f.K, n_mid = w[1], n_vlong = w[2], max_n = w[3];
@@ -573,7 +589,6 @@ int async_redo(AsyncFwd &f, std::map<int, hipStream_t> &streams) {
 }
 
 void resolver_main() {
-    std::map<int, hipStream_t> streams;
     std::unique_lock<std::mutex> lk(g_as_mu);
     for (;;) {
         bool pending = false, resolved = false;
@@ -607,8 +622,9 @@ void resolver_main() {
         }
         if (resolved) g_as_done.notify_all();
         if (todo) {
+            hipStream_t H = g_resolver_streams.count(todo->dev) ? g_resolver_streams[todo->dev] : nullptr;
             lk.unlock();
-            const int rc = async_redo(*todo, streams);
+            const int rc = async_redo(*todo, H);
             const std::string msg = rc ? g_err : std::string();
             __atomic_store_n(slot_h(todo->slot) + kGateWord, todo->seq, __ATOMIC_RELEASE);  // open the gate
             lk.lock();
@@ -621,7 +637,6 @@ void resolver_main() {
         if (pending) g_as_wake.wait_for(lk, std::chrono::microseconds(50));
         else g_as_wake.wait(lk);
     }
-    for (auto &kv : streams) (void)hipStreamDestroy(kv.second);
 }
 
 }  // namespace
@@ -687,7 +702,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     uint32_t *words_h = nullptr, *words_d = nullptr;
     if (mode == 2 && cap) {
         std::lock_guard<std::mutex> lk(g_as_mu);
-        if (async_init()) {
+        if (async_init() && resolver_stream(dev)) {
             const int slot = slot_acquire();
             if (slot >= 0) {
                 af = std::make_shared<AsyncFwd>();

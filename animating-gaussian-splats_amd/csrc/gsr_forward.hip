@@ -685,9 +685,9 @@ __global__ __launch_bounds__(512) void k_merge_pass(int T, const uint32_t *__res
 // holds the stream until the library's resolver thread has redone the post-scan kernels exactly on its
 // own stream and published `seq` in the forward's gate word (host-mapped) -- everything the caller
 // queues after the forward is ordered behind it.  When the speculation stood nothing waits.  A gate that
-// never opens (the resolver died) is abandoned after kGateTimeoutTicks with an error word set, so a
-// failure cannot hang the device.
-constexpr uint64_t kGateTimeoutTicks = 2000000000ull;  // s_memrealtime runs at 100 MHz: 20 s
+// never opens (the resolver died or is stuck) is abandoned after kGateTimeoutTicks with an error word
+// set, so a failure cannot hang the device.
+constexpr uint64_t kGateTimeoutTicks = 500000000ull;  // s_memrealtime runs at 100 MHz: 5 s
 __device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *err) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while ((int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {

@@ -102,6 +102,31 @@ def test_async_forward_stands_and_is_redone_bitwise(cuda):
     _same(held, exact_near)
 
 
+def test_async_redo_on_many_streams(cuda):
+    """Failed speculations on 8 caller streams (more streams than the process's hardware queues, so
+    they share queues): a redo must never queue behind the waiting forward's held queue -- the
+    resolver's stream has a hardware queue of its own.  Every forward completes with the exact image
+    (a stuck redo would trip the 5 s gate timeout and report an error)."""
+    P, W, H = 40_000, 320, 240
+    a = _cloud(cuda, P)
+    dense = dict(a, scales=a["scales"] * 3.0)
+    cam = S.render_settings(W, H, S.intrinsics(260.0, W, H), S.look_at(10, 0.1, 9.0), device=cuda, sh_degree=3)
+    ref = _forward(dense, cam, "exact")[1][1].clone()
+    streams = [torch.cuda.Stream() for _ in range(8)]
+    for k, st in enumerate(streams):
+        _C.speculation_stats(reset=True)
+        _forward(a, cam, "exact")  # sparse history: the dense forward below exceeds its capacity
+        torch.cuda.synchronize()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            info, out = _forward(dense, cam, "async")
+            busy = [torch.randn(1 << 20, device=cuda) * 2.0 for _ in range(4)]  # queued behind the forward
+        torch.cuda.synchronize()
+        assert info["pending"].resolve()[0] > 0 and info["pending"].redone, k
+        assert torch.equal(out[1], ref), k
+        del busy
+
+
 def test_async_forward_redo_with_long_lists(cuda):
     """A failed speculation whose tiles need the host-sized merge sort (> 4096 pairs): the resolver's
     redo runs the chunk sorts + merge passes with their temporary buffer."""
