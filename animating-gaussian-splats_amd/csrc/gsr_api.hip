@@ -474,19 +474,21 @@ uint32_t *gate_err_d() { return g_slot_d + (size_t)kAsyncSlots * kSlotWords; }
 void resolver_main();
 
 // The resolver's stream of each device.  A failed speculation holds the forward's stream in a
-// spinning wave until the redo on this stream is done, so this stream must never sit behind that wave
-// in a shared hardware queue (a process's streams share GPU_MAX_HW_QUEUES queues per priority): a
-// stream with a CU mask always gets a queue of its own (the mask enables every CU).  Created on the
+// spinning wave until the redo on this stream is done, so this stream must never wait for that wave:
+// (1) non-blocking (a blocking stream would wait for the legacy default stream, torch's default);
+// (2) not behind it in a hardware queue -- a process's streams share GPU_MAX_HW_QUEUES queues per
+// priority level, and the call-shape probe deadlocked when the resolver's normal-priority stream
+// shared the held stream's queue.  The resolver's stream therefore has the highest priority, a level
+// callers' streams do not use unless they ask for it.  (A CU-masked stream gets a queue of its own,
+// but HIP creates it blocking: the redo then waited for the held default stream.)  Created on the
 // caller's thread at the first asynchronous forward of the device (g_as_mu held).
 std::map<int, hipStream_t> g_resolver_streams;
 hipStream_t resolver_stream(int dev) {
     hipStream_t &h = g_resolver_streams[dev];
     if (h) return h;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
-    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-    if (hipExtStreamCreateWithCUMask(&h, (uint32_t)mask.size(), mask.data()) != hipSuccess) h = nullptr;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) hi = 0;
+    if (hipStreamCreateWithPriority(&h, hipStreamNonBlocking, hi) != hipSuccess) h = nullptr;
     return h;
 }
 
