@@ -444,7 +444,6 @@ struct AsyncFwd {
     void *spec_bin = nullptr;   // the caller's BINNING, laid out for `cap`
     hipEvent_t ev_scan = nullptr;  // recorded on `s` after k_bin_scan (the redo waits for it)
     int state = 0;              // 0 pending, 1 stood, 2 redo queued, 3 redone, -1 failed
-    uint32_t polls = 0;
     uint32_t K = 0;
     int layout = 0;
     void *bin = nullptr;        // the BINNING buffer the backward uses
@@ -590,54 +589,57 @@ int async_redo(AsyncFwd &f, hipStream_t H) {
     return GSR_OK;
 }
 
+// The resolver thread: takes the oldest unclassified forward, sleeps on its scan event (a
+// blocking-sync event: no polling, no CPU burned, no lock held), classifies it from the slot's words,
+// redoes it when the speculation failed, and drops released + resolved records.  Forwards whose
+// backward resolved them first are skipped.
 void resolver_main() {
     std::unique_lock<std::mutex> lk(g_as_mu);
     for (;;) {
-        bool pending = false, resolved = false;
-        std::shared_ptr<AsyncFwd> todo;
-        for (auto it = g_as.begin(); it != g_as.end();) {
-            AsyncFwd &f = *it->second;
-            if (f.state == 0 && __atomic_load_n(slot_h(f.slot), __ATOMIC_ACQUIRE) != kNoValue) {
-                async_classify(f);
-                resolved = resolved || f.state == 1;
-            }
-            if (f.state == 0) {
-                pending = true;
-                if (++f.polls % 20 == 0) {  // ~1 ms: a faulted stream never publishes K
-                    (void)hipSetDevice(f.dev);
-                    const hipError_t q = hipStreamQuery(f.s);
-                    if (q != hipErrorNotReady && __atomic_load_n(slot_h(f.slot), __ATOMIC_ACQUIRE) == kNoValue) {
-                        f.state = -1;
-                        f.err = q == hipSuccess ? std::string("num_rendered was not published")
-                                                : std::string("stream error before num_rendered was published: ") + hipGetErrorString(q);
-                        __atomic_store_n(slot_h(f.slot) + kGateWord, f.seq, __ATOMIC_RELEASE);
-                        resolved = true;
-                    }
-                }
-            }
-            if (f.state == 2 && !todo) todo = it->second;
-            if (f.released && (f.state == 1 || f.state == 3 || f.state == -1)) {
-                async_reap(it++);
-                continue;
-            }
-            ++it;
+        for (auto it = g_as.begin(); it != g_as.end();) {  // reap released, resolved records
+            const AsyncFwd &f = *it->second;
+            if (f.released && (f.state == 1 || f.state == 3 || f.state == -1)) async_reap(it++);
+            else ++it;
         }
-        if (resolved) g_as_done.notify_all();
-        if (todo) {
-            hipStream_t H = g_resolver_streams.count(todo->dev) ? g_resolver_streams[todo->dev] : nullptr;
-            lk.unlock();
-            const int rc = async_redo(*todo, H);
-            const std::string msg = rc ? g_err : std::string();
-            __atomic_store_n(slot_h(todo->slot) + kGateWord, todo->seq, __ATOMIC_RELEASE);  // open the gate
-            lk.lock();
-            todo->state = rc ? -1 : 3;
-            if (rc) { todo->err = msg; g_async_err = "asynchronous forward redo failed: " + msg; }
-            g_as_done.notify_all();
+        std::shared_ptr<AsyncFwd> next;
+        for (auto &kv : g_as)  // the oldest forward still to classify or redo
+            if ((kv.second->state == 0 || kv.second->state == 2) && (!next || kv.second->id < next->id)) next = kv.second;
+        if (!next) {
+            if (g_resolver_stop) break;
+            g_as_wake.wait(lk);
             continue;
         }
-        if (g_resolver_stop && !todo) break;
-        if (pending) g_as_wake.wait_for(lk, std::chrono::microseconds(50));
-        else g_as_wake.wait(lk);
+        if (next->state == 0) {
+            hipEvent_t ev = next->ev_scan;
+            const int dev = next->dev;
+            lk.unlock();
+            (void)hipSetDevice(dev);
+            const hipError_t r = hipEventSynchronize(ev);  // k_bin_scan done: its words are published
+            lk.lock();
+            if (next->state == 0) {
+                if (r != hipSuccess || __atomic_load_n(slot_h(next->slot), __ATOMIC_ACQUIRE) == kNoValue) {
+                    next->state = -1;
+                    next->err = r != hipSuccess ? std::string("stream error before num_rendered was published: ") +
+                                                      hipGetErrorString(r)
+                                                : std::string("num_rendered was not published");
+                    __atomic_store_n(slot_h(next->slot) + kGateWord, next->seq, __ATOMIC_RELEASE);
+                } else {
+                    async_classify(*next);
+                }
+                g_as_done.notify_all();
+            }
+            continue;
+        }
+        // state 2: redo the post-scan kernels exactly, then open the gate
+        hipStream_t H = g_resolver_streams.count(next->dev) ? g_resolver_streams[next->dev] : nullptr;
+        lk.unlock();
+        const int rc = async_redo(*next, H);
+        const std::string msg = rc ? g_err : std::string();
+        __atomic_store_n(slot_h(next->slot) + kGateWord, next->seq, __ATOMIC_RELEASE);  // open the gate
+        lk.lock();
+        next->state = rc ? -1 : 3;
+        if (rc) { next->err = msg; g_async_err = "asynchronous forward redo failed: " + msg; }
+        g_as_done.notify_all();
     }
 }
 
@@ -739,7 +741,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
             std::lock_guard<std::mutex> lk(g_as_mu);
             if (!g_as_evpool.empty()) { af->ev_scan = g_as_evpool.back(); g_as_evpool.pop_back(); }
         }
-        if (!af->ev_scan) HIP_TRY(hipEventCreateWithFlags(&af->ev_scan, hipEventDisableTiming));
+        if (!af->ev_scan) HIP_TRY(hipEventCreateWithFlags(&af->ev_scan, hipEventDisableTiming | hipEventBlockingSync));
         HIP_TRY(hipEventRecord(af->ev_scan, s));
     }
     const size_t spec_item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;

@@ -489,9 +489,11 @@ def step_stats(views_per_step, P, ms):
                                         for q in (75, 50, 25)]}
 
 
-def timed_steps(fn, steps, warmup, dev):
+def timed_steps(fn, steps, warmup, dev, host=None):
     """Run fn(it) warmup times, then `steps` times with an event on the current stream after each
-    step: per-step device intervals (ms)."""
+    step: per-step device intervals (ms).  ``host``: a list that receives each step's host time (ms,
+    the submitting thread's wall clock of the call): a step whose host time reaches its device time is
+    host-bound."""
     for it in range(warmup):
         fn(it)
     torch.cuda.synchronize()
@@ -499,7 +501,10 @@ def timed_steps(fn, steps, warmup, dev):
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     ev[0].record(s)
     for it in range(steps):
+        t = time.perf_counter()
         fn(warmup + it)
+        if host is not None:
+            host.append((time.perf_counter() - t) * 1e3)
         ev[it + 1].record(s)
     torch.cuda.synchronize()
     return [ev[i].elapsed_time(ev[i + 1]) for i in range(steps)]
@@ -535,8 +540,10 @@ def unchanged_call_site(steps, warmup, cfg, cams, views, dl, dev):
         losses.sum(dim=0).backward()
         delta.grad = None  # optimizer.zero_grad()
 
-    ms = timed_steps(one, steps, warmup, dev)
+    host = []
+    ms = timed_steps(one, steps, warmup, dev, host)
     out = {"features": "RGB (colors_precomp, as train.py renders)", "views_per_step": len(views(0)),
+           "host_ms_per_step_median": round(float(np.median(host)), 4),
            "threads": 1, "streams": "torch's current stream only", "steps": steps,
            "inputs": "non-leaf (frozen Gaussians, means/rotations = deepcopy.detach() + 0.01 delta, "
                      "per-view create_render_arguments)",
@@ -575,11 +582,13 @@ def c2_leg(steps, warmup, dev, nstreams=3):
         for v in leaves.values():
             v.grad = None
 
-    ms = timed_steps(one, steps, warmup, dev)
+    host = []
+    ms = timed_steps(one, steps, warmup, dev, host)
     rstep.close()
     out = {"workload": f"C2: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, 4 cameras per step, fwd+bwd, "
                        "view losses summed, one backward", "views_per_step": len(cams), "steps": steps,
-           "submission": f"one host thread, {nstreams} streams"}
+           "submission": f"one host thread, {nstreams} streams",
+           "host_ms_per_step_median": round(float(np.median(host)), 4)}
     out.update(step_stats(len(cams), cfg.P, ms))
     return out
 

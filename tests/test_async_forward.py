@@ -107,10 +107,10 @@ def test_async_redo_on_many_streams(cuda):
     they share queues): a redo must never queue behind the waiting forward's held queue -- the
     resolver's stream has a hardware queue of its own.  Every forward completes with the exact image
     (a stuck redo would trip the 5 s gate timeout and report an error)."""
-    P, W, H = 40_000, 320, 240
+    P, W, H = 60_000, 640, 480
     a = _cloud(cuda, P)
-    dense = dict(a, scales=a["scales"] * 3.0)
-    cam = S.render_settings(W, H, S.intrinsics(260.0, W, H), S.look_at(10, 0.1, 9.0), device=cuda, sh_degree=3)
+    dense = dict(a, scales=a["scales"] * 4.0)  # K 111873 -> 256884: past the capacity
+    cam = S.render_settings(W, H, S.intrinsics(500.0, W, H), S.look_at(30, 0.2, 9.0), device=cuda, sh_degree=3)
     ref = _forward(dense, cam, "exact")[1][1].clone()
     streams = [torch.cuda.Stream() for _ in range(8)]
     for k, st in enumerate(streams):

@@ -54,8 +54,8 @@ if args.profile:
     out["phase_ms"] = {ph: round(v[0] / max(v[1], 1), 4) for ph in bench.PHASES + ["host_forward", "host_wait_K", "host_backward"]
                        for v in [_C.profile_read(ph)]}
 out["wall_s"] = round(time.perf_counter() - t0, 2)
-out["unchanged"] = {k: u[k] for k in ("Msplats_per_s", "median_ms_per_step", "step_ms_quartiles")}
+out["unchanged"] = {k: u[k] for k in ("Msplats_per_s", "median_ms_per_step", "step_ms_quartiles", "host_ms_per_step_median")}
 if args.c2:
     c = bench.c2_leg(60, 10, dev)
-    out["c2"] = {k: c[k] for k in ("Msplats_per_s", "median_ms_per_step", "step_ms_quartiles")}
+    out["c2"] = {k: c[k] for k in ("Msplats_per_s", "median_ms_per_step", "step_ms_quartiles", "host_ms_per_step_median")}
 print(json.dumps(out), flush=True)

@@ -6,9 +6,10 @@ O=gpurun_out/r04/callshape.jsonl
 : > $O
 run() { timeout -k 10 180 "$@" >> $O 2> gpurun_out/r04/callshape.err; rc=$?; case $rc in 0|1) ;; *) echo "fatal rc=$rc"; exit $rc;; esac; }
 run python -u tools/callshape_probe.py all_on --c2 --profile
-run python -u tools/callshape_probe.py no_view_streams --profile
-run python -u tools/callshape_probe.py no_async --profile
+run python -u tools/callshape_probe.py no_view_streams --no-view-streams --profile
+run python -u tools/callshape_probe.py no_async --no-async --profile
 GSR_ITEMS_AUX=0 run python -u tools/callshape_probe.py no_items_aux
+GSR_ITEMS_AUX=0 run python -u tools/callshape_probe.py none --no-async --no-view-streams
 run python -u tools/callshape_probe.py no_async_no_vs --no-async --no-view-streams --profile
 run python -u tools/callshape_probe.py all_on_again
 cat $O
