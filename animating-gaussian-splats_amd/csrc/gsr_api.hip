@@ -97,9 +97,10 @@ struct Phase {
 // wait (stream order already holds).  Entries are dropped only once their event has completed (a
 // later writer then has nothing to wait for), so no pending write is ever forgotten, however many
 // gradient sets are in flight.
+std::vector<hipEvent_t> g_gw_evpool;  // (g_gw_mu) events of dropped entries, re-recorded by later writes
 struct GradEvent {
     hipEvent_t ev = nullptr;
-    ~GradEvent() { if (ev) (void)hipEventDestroy(ev); }
+    ~GradEvent() { if (ev) g_gw_evpool.push_back(ev); }  // destroyed under g_gw_mu (table updates)
 };
 struct GradWriter { hipStream_t s = nullptr; std::shared_ptr<GradEvent> ev; };
 std::mutex g_gw_mu;
@@ -126,7 +127,9 @@ hipError_t ordered_grad_write(const void *const *keys, int nkeys, hipStream_t s,
         if (nw < 16) waited[nw++] = e;
     }
     auto ev = std::make_shared<GradEvent>();
-    hipError_t r = hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming);
+    hipError_t r = hipSuccess;
+    if (!g_gw_evpool.empty()) { ev->ev = g_gw_evpool.back(); g_gw_evpool.pop_back(); }
+    else r = hipEventCreateWithFlags(&ev->ev, hipEventDisableTiming);
     if (r != hipSuccess) { ev->ev = nullptr; return r; }
     r = launch();
     if (r != hipSuccess) return r;

@@ -206,6 +206,11 @@ def _ptr(t):
     return t.data_ptr()
 
 
+def _bp(b):
+    """A workspace buffer given as a tensor (its data pointer) or as a device pointer (int)."""
+    return b if isinstance(b, int) else b.data_ptr()
+
+
 def _f32(t):
     return t.contiguous() if t is not None and t.numel() else t
 
@@ -231,13 +236,15 @@ _PREALLOC_ON = os.environ.get("GSR_PREALLOC", "1") != "0"  # 0: every request th
 class _PreAllocator:
     """Buffers sized on the host before the native call and handed out by gsr_prealloc_alloc (C),
     so the call makes no ctypes callback (which would re-acquire the interpreter lock while other
-    threads submit their views) unless a request exceeds them.  ``sizes``: {gsr_buffer: bytes};
-    buffers given as one list are carved from ONE allocation (they share its lifetime)."""
+    threads submit their views) unless a request exceeds them.  ``groups``: lists of (gsr_buffer,
+    bytes); the buffers of one list are carved from ONE allocation (they share its lifetime).  After the
+    call: ``ptrs`` (gsr_buffer -> device pointer handed out), ``bases`` (the allocations backing them,
+    what keeps them alive) and, built on first use, ``buffers`` (gsr_buffer -> uint8 tensor view)."""
 
     def __init__(self, device, groups):
         self.device = device
         self.pa = _Prealloc()
-        self.given = {}
+        self.given = {}  # which -> (base tensor, offset, bytes)
         for group in groups if _PREALLOC_ON else ():
             offs, total = [], 0
             for which, nbytes in group:
@@ -246,15 +253,16 @@ class _PreAllocator:
             if total == 0:
                 continue
             buf = torch.empty(total, dtype=torch.uint8, device=device)
+            base = buf.data_ptr()
             for which, o, nbytes in offs:
                 if nbytes > 0:
-                    t = buf.narrow(0, o, int(nbytes))
-                    self.given[which] = t
-                    self.pa.ptr[which] = t.data_ptr()
+                    self.given[which] = (buf, o, int(nbytes))
+                    self.pa.ptr[which] = base + o
                     self.pa.bytes[which] = int(nbytes)
         self.pa.fallback = _FALLBACK_FN
         self.cb = _PREALLOC_FN
         self.ctx = ctypes.byref(self.pa)
+        self._views = None
 
     def __enter__(self):
         self.prev = getattr(_tls, "buffers", None), getattr(_tls, "device", None)
@@ -264,10 +272,35 @@ class _PreAllocator:
     def __exit__(self, *exc):
         got = _tls.buffers
         _tls.buffers, _tls.device = self.prev
-        # what the call took: the pre-allocated tensors it was handed, and the fallback's
-        self.buffers = {w: t for w, t in self.given.items() if (self.pa.used >> w) & 1}
-        self.buffers.update(got)
+        # what the call took: the pre-allocated buffers it was handed, and the fallback's
+        used = self.pa.used
+        self.taken = {w: g for w, g in self.given.items() if (used >> w) & 1}
+        self.fallback = got
+        self.ptrs = {w: self.pa.ptr[w] for w in self.taken}
+        self.ptrs.update({w: t.data_ptr() for w, t in got.items()})
+        bases = {id(g[0]): g[0] for g in self.taken.values()}
+        bases.update({id(t): t for t in got.values()})
+        self.bases = list(bases.values())
         return False
+
+    def base_of(self, which):
+        """The allocation backing buffer `which` (to record it on another stream)."""
+        if which in self.fallback:
+            return self.fallback[which]
+        g = self.taken.get(which)
+        return g[0] if g is not None else None
+
+    @property
+    def buffers(self):
+        if self._views is None:
+            v = {w: b.narrow(0, o, n) for w, (b, o, n) in self.taken.items()}
+            v.update(self.fallback)
+            self._views = v
+        return self._views
+
+
+_get_device = torch._C._cuda_getDevice
+_raw_stream = torch._C._cuda_getCurrentRawStream
 
 
 class _device_guard:
@@ -275,11 +308,11 @@ class _device_guard:
     the current device); free when it already is, which is the common case."""
 
     def __init__(self, dev):
-        self.idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        self.idx = dev.index if dev.index is not None else _get_device()
         self.prev = None
 
     def __enter__(self):
-        cur = torch.cuda.current_device()
+        cur = _get_device()
         if cur != self.idx:
             self.prev = cur
             torch.cuda.set_device(self.idx)
@@ -292,16 +325,32 @@ class _device_guard:
 
 
 def _stream_ptr(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The raw current HIP stream of `device` (torch's current stream)."""
+    return ctypes.c_void_p(_raw_stream(device.index if device.index is not None else _get_device()))
+
+
+_CAM_CACHE = {}
+_CAM_CACHE_MAX = 512
 
 
 def _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, campos, bg,
             prefiltered, keep):
     # the matrices and campos go in as they are (strided views included: the reference's viewmatrix
-    # is a transposed view, campos a column slice) -- no per-call device copy
+    # is a transposed view, campos a column slice) -- no per-call device copy.  The struct of a camera
+    # whose tensors need no conversion is cached by the tensors' identity and data pointers (train.py
+    # renders the same View.render_settings every step).
+    key = (id(viewmatrix), id(projmatrix), id(campos), id(bg), image_width, image_height, tan_fovx, tan_fovy,
+           prefiltered)
+    e = _CAM_CACHE.get(key)
+    if e is not None:
+        cam, refs, ptrs = e
+        if (refs[0] is viewmatrix and refs[1] is projmatrix and refs[2] is campos and refs[3] is bg and
+                ptrs == (viewmatrix.data_ptr(), projmatrix.data_ptr(),
+                         campos.data_ptr() if campos is not None else 0, bg.data_ptr())):
+            return cam
     vm, vs = _mat16(viewmatrix)
     pm, ps = _mat16(projmatrix)
-    bg_ = bg.contiguous().float()
+    bg_ = bg if bg.dtype == torch.float32 and bg.is_contiguous() else bg.contiguous().float()
     cp, cs = None, 0
     if campos is not None and campos.numel():
         cp = campos if campos.dtype == torch.float32 and campos.dim() == 1 else campos.reshape(-1).float()
@@ -313,18 +362,25 @@ def _camera(viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_widt
     cam.viewmatrix_stride[0], cam.viewmatrix_stride[1] = vs
     cam.projmatrix_stride[0], cam.projmatrix_stride[1] = ps
     cam.campos_stride = cs
+    if vm is viewmatrix and pm is projmatrix and bg_ is bg and (cp is campos):  # nothing converted
+        if len(_CAM_CACHE) >= _CAM_CACHE_MAX:
+            _CAM_CACHE.clear()
+        _CAM_CACHE[key] = (cam, (viewmatrix, projmatrix, campos, bg),
+                           (viewmatrix.data_ptr(), projmatrix.data_ptr(),
+                            campos.data_ptr() if campos is not None else 0, bg.data_ptr()))
     return cam
 
 
 def _mat16(m):
-    """A 4x4 camera matrix ((4, 4) or (1, 4, 4), any strides) as (fp32 tensor, (row, col) strides)."""
+    """A 4x4 camera matrix ((4, 4) or (1, 4, 4), any strides) as (fp32 tensor whose data pointer is
+    element [0][0], (row, col) element strides) -- the tensor itself when it needs no conversion."""
     if m.numel() != 16:
         raise RuntimeError("viewmatrix/projmatrix must hold 16 floats")
     if m.dtype != torch.float32:
         m = m.float()
-    m2 = m.reshape(4, 4) if m.dim() != 3 else m[0]
-    if m2.dim() != 2 or m2.shape != (4, 4):
-        raise RuntimeError("viewmatrix/projmatrix must hold 16 floats")
+    if m.shape in ((4, 4), (1, 4, 4)):
+        return m, (m.stride(-2), m.stride(-1))
+    m2 = m.reshape(4, 4)
     return m2, (m2.stride(0), m2.stride(1))
 
 
@@ -348,13 +404,14 @@ class AsyncForward:
     (the BINNING buffer is the forward's own, or the library's when the speculation was redone);
     ``ready()`` says whether that would return without waiting.  The handle is released when this
     object is collected (after the backward that holds it)."""
-    __slots__ = ("handle", "_res", "__weakref__")
+    __slots__ = ("handle", "_res")
 
     def __init__(self, handle):
         self.handle = int(handle)
         self._res = None
-        import weakref
-        weakref.finalize(self, _release_async, self.handle)
+
+    def __del__(self):
+        _release_async(self.handle)
 
     def ready(self):
         return self._res is not None or load_library().gsr_forward_query(self.handle) > 0
@@ -396,6 +453,22 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     ``speculated`` and ``pending``.  ``nonblocking``: gsr_forward_async -- with a capacity from the
     pair-count history the call returns without reading num_rendered back; ``num_rendered`` is then
     -1 and ``info["pending"]`` an ``AsyncForward`` whose ``resolve()`` gives what the backward needs."""
+    fi, color, radii, depth, alloc, pending = _forward(
+        background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+        projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, activations,
+        prepare_backward, speculate, nonblocking)
+    if info is not None:
+        info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated),
+                    pending=pending)
+    b = alloc.buffers
+    return fi.num_rendered, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
+
+
+def _forward(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+             projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, activations,
+             prepare_backward, speculate, nonblocking):
+    """rasterize_gaussians without the buffer views: returns (gsr_forward_info, color, radii, depth,
+    the _PreAllocator (``ptrs`` / ``bases`` of GEOM, BINNING, IMAGE), the AsyncForward or None)."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
@@ -424,13 +497,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                                                color.data_ptr(), depth.data_ptr(), radii.data_ptr() if P else None,
                                                int(bool(speculate)), ctypes.byref(fi), _stream_ptr(dev)))
     pending = AsyncForward(fi.pending) if fi.pending else None
-    b = alloc.buffers
-    if fi.aux_stream and GSR_BUF_BINNING in b:  # the item list is written on the library's auxiliary
-        b[GSR_BUF_BINNING].record_stream(_external_stream(fi.aux_stream, dev))  # stream: no early reuse
-    if info is not None:
-        info.update(num_rendered=fi.num_rendered, binning_layout=fi.binning_layout, speculated=bool(fi.speculated),
-                    pending=pending)
-    return fi.num_rendered, color, radii, b[GSR_BUF_GEOM], b[GSR_BUF_BINNING], b[GSR_BUF_IMAGE], depth
+    if fi.aux_stream:  # the item list is written into BINNING on the library's auxiliary stream: no early reuse
+        bb = alloc.base_of(GSR_BUF_BINNING)
+        if bb is not None:
+            bb.record_stream(_external_stream(fi.aux_stream, dev))
+    return fi, color, radii, depth, alloc, pending
 
 
 _EXT_STREAMS = {}
@@ -527,7 +598,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     alloc = _PreAllocator(dev, [[(GSR_BUF_SCRATCH, L.gsr_scratch_bytes(int(R), W, H))]])
     with _device_guard(dev), alloc:
         _check(L.gsr_backward(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
-                              geomBuffer.data_ptr(), binning_ptr or binningBuffer.data_ptr(), imageBuffer.data_ptr(),
+                              _bp(geomBuffer), binning_ptr or _bp(binningBuffer), _bp(imageBuffer),
                               dpix.data_ptr(), None, alloc.cb, alloc.ctx, ctypes.byref(grads), _stream_ptr(dev)))
     return out
 
@@ -558,8 +629,7 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
                                 [(GSR_BUF_SUMS, L.gsr_sums_bytes(P))]])
     with _device_guard(dev), alloc:
         _check(L.gsr_backward_render(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),
-                                     geomBuffer.data_ptr(), binning_ptr or binningBuffer.data_ptr(),
-                                     imageBuffer.data_ptr(),
+                                     _bp(geomBuffer), binning_ptr or _bp(binningBuffer), _bp(imageBuffer),
                                      dpix.data_ptr(), alloc.cb, alloc.ctx, _stream_ptr(dev)))
     return alloc.buffers[GSR_BUF_SUMS]
 
@@ -572,7 +642,8 @@ def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations
     (slot 0, dL/dmeans2D, is None: each view's goes to its own array; ``needed`` as in
     ``rasterize_gaussians_backward``).  ``views``: dicts with the
     view's ``viewmatrix``, ``projmatrix``, ``tanfovx``, ``tanfovy``, ``image_height``, ``image_width``,
-    ``campos``, ``bg``, its ``radii``, ``geomBuffer``, ``scratch`` (from
+    ``campos``, ``bg``, its ``radii``, ``geomBuffer`` (a tensor or a device pointer, then ``keep``: the
+    tensors backing it), ``scratch`` (from
     ``rasterize_gaussians_backward_render``) and ``num_rendered``, and optionally ``means2D_grad``, a
     contiguous (P, 3) fp32 tensor receiving its screen-space gradient (added into when
     ``accumulate_means2D``).  ``overwrite``: output slots whose ``accumulate_into`` tensor is written
@@ -600,9 +671,10 @@ def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations
             if tuple(m2.shape) != (P, 3) or m2.dtype != torch.float32 or not m2.is_contiguous() or m2.device != dev:
                 raise RuntimeError(f"views[{k}]['means2D_grad']: expected a contiguous float32 ({P}, 3) tensor on {dev}")
             m2.record_stream(cs)
-        for t in (v["radii"], v["geomBuffer"], v["scratch"]):  # read on this stream, maybe allocated
-            t.record_stream(cs)                                 # on the view's
-        vg[k] = _ViewGrad(ctypes.pointer(cam), v["radii"].data_ptr(), v["geomBuffer"].data_ptr(),
+        for t in (v["radii"], v["scratch"], *v.get("keep", ()),  # read on this stream, maybe allocated
+                  *((v["geomBuffer"],) if isinstance(v["geomBuffer"], torch.Tensor) else ())):  # on the view's
+            t.record_stream(cs)
+        vg[k] = _ViewGrad(ctypes.pointer(cam), v["radii"].data_ptr(), _bp(v["geomBuffer"]),
                           v["scratch"].data_ptr(), int(v["num_rendered"]),
                           m2.data_ptr() if m2 is not None else None, int(bool(v.get("accumulate_means2D"))))
     grads = _Grads(*[t.data_ptr() if t is not None and t.numel() else None for t in out], acc_bits)

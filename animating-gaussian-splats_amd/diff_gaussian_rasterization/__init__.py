@@ -185,6 +185,12 @@ def set_async_forward(on: bool) -> bool:
     return prev
 
 
+def _buffer_ptrs(alloc):
+    """(GEOM, BINNING, IMAGE) device pointers of a forward's workspaces (_C._forward)."""
+    p = alloc.ptrs
+    return p[_C.GSR_BUF_GEOM], p[_C.GSR_BUF_BINNING], p[_C.GSR_BUF_IMAGE]
+
+
 def _resolved(ctx):
     """(num_rendered, binning_layout, binning pointer or None) of the forward behind ``ctx``: an
     asynchronous forward is resolved here (waits for its pair count if the GPU has not produced it)."""
@@ -282,7 +288,7 @@ def _run_group(grp, created, post):
             created.discard(id(grp["targets"][k].leaf))
 
 
-def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn):
+def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn, keep=()):
     """Queue this view for the end-of-pass per-Gaussian backward when every gradient it must produce
     can go into a leaf's .grad; returns True when queued (the Function then returns None for all).
     ``render_fn()`` runs the view's per-pixel half and returns ``(SUMS buffer, num_rendered)``.  When
@@ -323,7 +329,8 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
     view = {"viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix, "tanfovx": rs.tanfovx,
             "tanfovy": rs.tanfovy, "image_height": rs.image_height, "image_width": rs.image_width,
             "campos": rs.campos, "bg": rs.bg, "radii": radii, "geomBuffer": geomBuffer, "scratch": scratch,
-            "num_rendered": K, "means2D_grad": targets[0], "accumulate_means2D": True, "stream": stream}
+            "num_rendered": K, "means2D_grad": targets[0], "accumulate_means2D": True, "stream": stream,
+            "keep": keep}
     if scratch is None:
         view["render_fn"] = render_fn
     with _pending_lock:
@@ -344,9 +351,8 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
     args = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
-    bridged = _bridged_inputs(args)
-    if bridged:
-        return _on_view_stream(args, bridged, raster_settings)
+    if _view_stream_call(args):
+        return _on_view_stream(args, raster_settings)
     return _RasterizeGaussians.apply(*args, raster_settings, torch.is_grad_enabled())
 
 
@@ -355,19 +361,20 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
 # (create_render_arguments: normalize / sigmoid / exp / zeros + 0, shared.py:29-42) and one backward of
 # the summed losses (train.py:402-418).  Every gradient the rasterizer returns then goes to a node of the
 # caller's graph that ran on C, and the autograd engine makes C wait for the producing stream the moment
-# it hands a gradient over (InputBuffer::add).  It hands them over right after each view's backward node
-# returns, and it runs the nodes by descending sequence number: view k's consumers (its normalize etc.)
-# come before view k-1's loss backward.  So the views' backward kernels would run strictly one after
-# another, whatever stream they were queued on.
+# it hands a gradient over (InputBuffer::add), i.e. right after the producing node returns.  The engine
+# runs ready nodes by descending sequence number, so the rasterizer node of view k (created after view
+# k-1's loss) runs before view k-1's loss backward and C waits for it before that loss backward: the
+# views' backward kernels would run strictly one after another, whatever stream they were queued on.
 # Here each such view runs on one of the library's view streams L (round robin): L waits for C, the
 # forward is queued on L, C waits for L before the outputs are used (the forward stays ordered as the
-# caller wrote it).  The non-leaf inputs go through a _StreamBridge node created by a helper thread --
-# sequence numbers are per thread, so the bridge has the lowest priority of the pass: the engine runs
-# every view's loss backward and rasterizer backward (queued on that view's L, so they overlap on the
-# GPU) before any bridge, and each bridge then hands its view's gradients to C (record_stream + wait).
-# Leaf inputs are not bridged (the backward adds into their .grad in place on L); the end of the pass
-# makes C wait for every L used.  Results are bitwise those of one stream: every gradient write is
-# ordered (gsr_grad_fence / ordered_grad_write) and each consumer waits for its producer.
+# caller wrote it).  The rasterizer node itself is created by a helper thread: sequence numbers are per
+# thread, so it has the lowest priority of the pass -- the engine runs every view's loss backward first,
+# then the rasterizer nodes, each queuing its view's backward on that view's L right away (they overlap
+# on the GPU), and the caller's consumers on C wait for each L as the engine hands the gradients over.
+# Gradients made on L and read on C are record_stream'ed on C; leaf gradients are added into .grad in
+# place on L, and the end of the pass makes C wait for every L it used.  Results are bitwise those of
+# one stream: every gradient write is ordered (ordered_grad_write) and each consumer waits for its
+# producer.
 _VIEW_STREAMS = {"on": os.environ.get("GSR_VIEW_STREAMS", "1") != "0", "n": 3, "pool": {}, "next": {}}
 
 
@@ -378,13 +385,12 @@ def set_view_streams(on: bool) -> bool:
     return prev
 
 
-def _bridged_inputs(args):
-    """Indices of the inputs a view-stream render bridges (non-leaf, requiring grad), or () when the
-    call takes the caller's stream (disabled, no grad, no such input, CPU tensors)."""
+def _view_stream_call(args):
+    """Does this call take a view stream: enabled, grad mode, GPU inputs, and an input that is not a leaf
+    but requires grad (its gradient goes to a node of the caller's graph)."""
     if not _VIEW_STREAMS["on"] or not torch.is_grad_enabled() or not args[0].is_cuda:
-        return ()
-    return tuple(i for i, t in enumerate(args)
-                 if isinstance(t, torch.Tensor) and t.numel() and t.requires_grad and not t.is_leaf)
+        return False
+    return any(isinstance(t, torch.Tensor) and t.requires_grad and not t.is_leaf and t.numel() for t in args)
 
 
 def _view_stream(dev):
@@ -398,33 +404,14 @@ def _view_stream(dev):
     return pool[k]
 
 
-class _StreamBridge(torch.autograd.Function):
-    """Identity over a view's non-leaf inputs, created on the view's stream by the helper thread (low
-    sequence number: the engine runs it after every other ready node).  Its backward hands the view's
-    gradients to the caller's stream."""
-
-    @staticmethod
-    def forward(ctx, caller, *xs):
-        ctx.caller = caller
-        return tuple(x.view_as(x) for x in xs)
-
-    @staticmethod
-    def backward(ctx, *gs):
-        for g in gs:
-            if g is not None:
-                g.record_stream(ctx.caller)  # produced on this view's stream, consumed on the caller's
-        ctx.caller.wait_stream(torch.cuda.current_stream())
-        return (None,) + gs
-
-
-class _BridgeThread:
-    """The helper thread that creates _StreamBridge nodes (its autograd sequence numbers stay far below
-    the caller's); one synchronous hand-off per view-stream render."""
+class _HelperThread:
+    """The thread that creates the view-stream rasterizer nodes (its autograd sequence numbers stay far
+    below the caller's, which makes dozens of nodes per view); one synchronous hand-off per render."""
 
     def __init__(self):
         import queue
-        self.q = queue.Queue()
-        self.t = threading.Thread(target=self._run, name="gsr-bridge", daemon=True)
+        self.q = queue.SimpleQueue()
+        self.t = threading.Thread(target=self._run, name="gsr-views", daemon=True)
         self.t.start()
 
     def _run(self):
@@ -434,53 +421,45 @@ class _BridgeThread:
                 box["out"] = job()
             except BaseException as e:  # noqa: BLE001 - re-raised in the caller
                 box["err"] = e
-            done.set()
+            done.release()
 
     def call(self, job):
-        done, box = threading.Event(), {}
+        done, box = threading.Lock(), {}
+        done.acquire()
         self.q.put((job, done, box))
-        done.wait()
+        done.acquire()  # released by the helper when the job is done
         if "err" in box:
             raise box["err"]
         return box["out"]
 
 
-_bridge_thread = None
-_bridge_lock = threading.Lock()
+_helper = None
+_helper_lock = threading.Lock()
 _sync_tasks = {}  # graph task -> the (caller stream, view streams) its end-of-pass callback joins
 
 
-def _bridge(xs, caller, L, dev):
-    global _bridge_thread
-    with _bridge_lock:
-        if _bridge_thread is None:
-            _bridge_thread = _BridgeThread()
-
-    def job():
-        with torch.enable_grad(), torch.cuda.device(dev), torch.cuda.stream(L):
-            return _StreamBridge.apply(caller, *xs)
-    out = _bridge_thread.call(job)
-    return out if isinstance(out, tuple) else (out,)
-
-
-def _on_view_stream(args, bridged, rs):
+def _on_view_stream(args, rs):
+    global _helper
     dev = args[0].device
     C = torch.cuda.current_stream(dev)
     L = _view_stream(dev)
     L.wait_stream(C)  # the caller's inputs (activations) are ready on L
     for t in args:
         if t.numel() and t.is_cuda:
-            t.record_stream(L)  # read on L (forward and backward) -- no early reuse on C
-    xs = list(args)
-    out = _bridge([args[i] for i in bridged], C, L, dev)
-    for i, t in zip(bridged, out):
-        xs[i] = t
-    _view_tls.cur = (C, L)  # read by the Function's forward (same thread, synchronous)
-    try:
-        with torch.cuda.stream(L):
-            color, radii, depth = _RasterizeGaussians.apply(*xs, rs, True)
-    finally:
-        _view_tls.cur = None
+            t.record_stream(L)  # read on L (forward and backward): no early reuse on C
+    if _helper is None:
+        with _helper_lock:
+            if _helper is None:
+                _helper = _HelperThread()
+
+    def job():
+        with torch.enable_grad(), torch.cuda.device(dev), torch.cuda.stream(L):
+            _view_tls.cur = (C, L)  # read by the Function's forward (this thread, synchronous)
+            try:
+                return _RasterizeGaussians.apply(*args, rs, True)
+            finally:
+                _view_tls.cur = None
+    color, radii, depth = _helper.call(job)
     for t in (color, radii, depth):
         t.record_stream(C)
     C.wait_stream(L)  # the outputs are used on the caller's stream
@@ -497,7 +476,7 @@ def _view_stream_backward(ctx):
     task = torch._C._current_graph_task_id()
     if task < 0:
         return
-    with _bridge_lock:
+    with _helper_lock:
         ent = _sync_tasks.get(task)
         new = ent is None
         if new:
@@ -505,7 +484,7 @@ def _view_stream_backward(ctx):
         ent[1].add(ctx.view_stream)
     if new:
         def join():
-            with _bridge_lock:
+            with _helper_lock:
                 caller, streams = _sync_tasks.pop(task, (None, ()))
             for st in streams:
                 caller.wait_stream(st)
@@ -523,21 +502,20 @@ class _RasterizeGaussians(torch.autograd.Function):
         # a backward can follow (grad mode at the call, an input requiring grad): the forward
         # prepares it
         ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)
-        info = {}
-        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = \
-            _C.rasterize_gaussians(*args, prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info,
-                                   nonblocking=_defer["async"])
+        fi, color, radii, depth, alloc, pending = _C._forward(
+            *args, 0, ctx.prep, _defer["speculate"], _defer["async"])
         ctx.raster_settings = rs
-        ctx.num_rendered = num_rendered
-        ctx.binning_layout = info["binning_layout"]
-        ctx.pending = info["pending"]  # an asynchronous forward: resolved by the backward
+        ctx.num_rendered = fi.num_rendered
+        ctx.binning_layout = fi.binning_layout
+        ctx.pending = pending  # an asynchronous forward: resolved by the backward
+        ctx.bufs = _buffer_ptrs(alloc)  # GEOM, BINNING, IMAGE device pointers (the bases are saved)
         ctx.view_caller, ctx.view_stream = getattr(_view_tls, "cur", None) or (None, None)
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
         ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
         ctx.tensor_pos = _tensor_positions((means3D, means2D, sh, colors_precomp, opacities, scales,
                                             rotations, cov3Ds_precomp))
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
-                              geomBuffer, binningBuffer, imgBuffer)
+                              *alloc.bases)
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)  # no zero-filled gradients for the unused depth output
         return color, radii, depth
@@ -549,8 +527,11 @@ class _RasterizeGaussians(torch.autograd.Function):
         if grad_out_color is None:  # only depth was used: it carries no gradient (-w-depth)
             return (None,) * 10
         rs = ctx.raster_settings
-        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer,
-         binningBuffer, imgBuffer) = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh = saved[:7]
+        bases = saved[7:]
+        geomBuffer, binningBuffer, imgBuffer = ctx.bufs
+
         def args_kw():  # the forward's pair count and BINNING (an asynchronous forward resolves here)
             K, layout, bptr = _resolved(ctx)
             return ((rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
@@ -565,7 +546,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         nodes = _input_nodes(ctx, inputs)
         gauss = (means3D, colors_precomp, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
                  rs.sh_degree, 0)
-        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad, render_half):
+        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, ctx.needs_input_grad, render_half, bases):
             return (None,) * 10  # every gradient is added into its leaf's .grad at the end of the pass
         args, kw = args_kw()
         need = [ctx.needs_input_grad[i] for i in inputs]
@@ -574,6 +555,10 @@ class _RasterizeGaussians(torch.autograd.Function):
         for k, t in enumerate(acc):
             if t is not None:
                 g[k] = None  # already accumulated into the leaf's .grad
+        if ctx.view_stream is not None:  # made on the view stream, read by the caller's graph on C
+            for t in g:
+                if t is not None:
+                    t.record_stream(ctx.view_caller)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp,
          grad_sh, grad_scales, grad_rotations) = g
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities,
@@ -645,21 +630,19 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         rs = raster_settings
         empty = torch.empty(0, device=means.device)
         ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)  # a backward can follow
-        info = {}
-        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, depth = _C.rasterize_gaussians(
+        fi, color, radii, depth, alloc, pending = _C._forward(
             rs.bg, means, colors, opacity_logits, log_scales, quaternions, rs.scale_modifier, empty,
             rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
-            rs.sh_degree, rs.campos, rs.prefiltered, activations=_C.ACT_ALL,
-            prepare_backward=ctx.prep, speculate=_defer["speculate"], info=info, nonblocking=_defer["async"])
+            rs.sh_degree, rs.campos, rs.prefiltered, _C.ACT_ALL, ctx.prep, _defer["speculate"], _defer["async"])
         ctx.raster_settings = rs
-        ctx.num_rendered = num_rendered
-        ctx.binning_layout = info["binning_layout"]
-        ctx.pending = info["pending"]
+        ctx.num_rendered = fi.num_rendered
+        ctx.binning_layout = fi.binning_layout
+        ctx.pending = pending
+        ctx.bufs = _buffer_ptrs(alloc)
         ctx.opacity_shape = opacity_logits.shape
         ctx.leaves = (means2D, colors, opacity_logits, means, None, sh, log_scales, quaternions)
         ctx.tensor_pos = _tensor_positions((means, means2D, sh, colors, opacity_logits, log_scales, quaternions))
-        ctx.save_for_backward(colors, means, log_scales, quaternions, radii, sh, geomBuffer,
-                              binningBuffer, imgBuffer)
+        ctx.save_for_backward(colors, means, log_scales, quaternions, radii, sh, *alloc.bases)
         ctx.mark_non_differentiable(radii)
         ctx.set_materialize_grads(False)
         return color, radii, depth
@@ -669,8 +652,10 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         if grad_out_color is None:
             return (None,) * 9
         rs = ctx.raster_settings
-        colors, means, log_scales, quaternions, radii, sh, geomBuffer, binningBuffer, imgBuffer = \
-            ctx.saved_tensors
+        saved = ctx.saved_tensors
+        colors, means, log_scales, quaternions, radii, sh = saved[:6]
+        bases = saved[6:]
+        geomBuffer, binningBuffer, imgBuffer = ctx.bufs
         empty = torch.empty(0, device=means.device)
         need = ctx.needs_input_grad
         inputs = (1, 3, 4, 0, None, 2, 5, 6)  # input index of each leaf (grad output order; no cov3D)
@@ -684,7 +669,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,
                 rs.sh_degree, rs.campos, geomBuffer, K, binningBuffer, imgBuffer,
                 activations=_C.ACT_ALL, prepare_backward=ctx.prep, binning_layout=layout, binning_ptr=bptr), K
-        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, need, render_half):
+        if _try_defer(ctx, gauss, radii, geomBuffer, inputs, nodes, need, render_half, bases):
             return (None,) * 9
         K, layout, bptr = _resolved(ctx)
         acc = [_accumulation_target(t, node) if i is not None and need[i] else None

@@ -31,28 +31,31 @@ class _Tag(torch.autograd.Function):
 
 
 def test_helper_thread_nodes_run_after_the_callers_nodes():
+    """train.py's graph: per view an activation, the rasterizer node (made by the helper thread), a loss;
+    the losses stacked and summed.  The engine must run every view's loss backward before any rasterizer
+    node, and the rasterizer nodes before their activations' backward."""
     log = []
-    helper = dgr._BridgeThread()
+    helper = dgr._HelperThread()
     p = torch.randn(8, requires_grad=True)
     # a training program's thread has made many autograd nodes before (train.py: the deformation
     # network, every earlier step); the helper makes one per view-stream render
     for _ in range(200):
         (p * 1.0).sum()
     losses = []
-    for k in range(4):
-        act = p * 2.0
+    for k in range(5):
+        act = _Tag.apply(p * 2.0, log, f"act{k}")
+
         def make(act=act, k=k):
             with torch.enable_grad():
-                return _Tag.apply(act, log, f"bridge{k}")
-        b = helper.call(make)
-        r = _Tag.apply(b * 1.0, log, f"rast{k}")
+                return _Tag.apply(act, log, f"rast{k}")
+        r = helper.call(make)
         losses.append(_Tag.apply(r.sum(), log, f"loss{k}"))
     torch.stack(losses).sum().backward()
-    rast = [i for i, n in enumerate(log) if n.startswith("rast")]
-    bridge = [i for i, n in enumerate(log) if n.startswith("bridge")]
-    assert len(rast) == len(bridge) == 4
-    assert max(rast) < min(bridge), log  # every view's rasterizer backward before any bridge
-    assert torch.equal(p.grad, torch.full_like(p, 8.0))
+    pos = {n: i for i, n in enumerate(log)}
+    assert max(pos[f"loss{k}"] for k in range(5)) < min(pos[f"rast{k}"] for k in range(5)), log
+    assert [n for n in log if n.startswith("rast")] == [f"rast{k}" for k in (4, 3, 2, 1, 0)], log
+    assert all(pos[f"rast{k}"] < pos[f"act{k}"] for k in range(5)), log
+    assert torch.equal(p.grad, torch.full_like(p, 10.0))
 
 
 def _train_step(cams, base, dl, delta):
