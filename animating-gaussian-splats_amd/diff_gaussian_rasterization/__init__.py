@@ -438,12 +438,29 @@ _helper_lock = threading.Lock()
 _sync_tasks = {}  # graph task -> the (caller stream, view streams) its end-of-pass callback joins
 
 
+_STREAMS = {}  # raw HIP stream -> torch Stream object (torch.cuda.current_stream builds a new one per call)
+_EVENTS = {}   # (caller stream, view stream) -> (fork event, join event), re-recorded every call
+
+
+def _current_stream(idx):
+    raw = _C._raw_stream(idx)
+    st = _STREAMS.get(raw)
+    if st is None:
+        st = _STREAMS[raw] = torch.cuda.current_stream(idx)
+    return st
+
+
 def _on_view_stream(args, rs):
     global _helper
     dev = args[0].device
-    C = torch.cuda.current_stream(dev)
+    idx = dev.index if dev.index is not None else _C._get_device()
+    C = _current_stream(idx)
     L = _view_stream(dev)
-    L.wait_stream(C)  # the caller's inputs (activations) are ready on L
+    evs = _EVENTS.get((C.cuda_stream, L.cuda_stream))
+    if evs is None:
+        evs = _EVENTS[(C.cuda_stream, L.cuda_stream)] = (torch.cuda.Event(), torch.cuda.Event())
+    evs[0].record(C)
+    L.wait_event(evs[0])  # the caller's inputs (activations) are ready on L
     for t in args:
         if t.numel() and t.is_cuda:
             t.record_stream(L)  # read on L (forward and backward): no early reuse on C
@@ -462,7 +479,8 @@ def _on_view_stream(args, rs):
     color, radii, depth = _helper.call(job)
     for t in (color, radii, depth):
         t.record_stream(C)
-    C.wait_stream(L)  # the outputs are used on the caller's stream
+    evs[1].record(L)
+    C.wait_event(evs[1])  # the outputs are used on the caller's stream
     return color, radii, depth
 
 
