@@ -235,6 +235,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.tile_count = (uint32_t *)(base + L.tile_count); a.tile_cursor = (uint32_t *)(base + L.tile_cursor);
     a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
     a.meta = (uint32_t *)(base + L.meta); a.chunk_off = (uint32_t *)(base + L.chunk_off);
+    a.items_ws = (uint32_t *)(base + L.items_ws);
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K, a.P);
@@ -356,9 +357,12 @@ void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
 // after the render; the backward's render half waits for it (items_join) before k_render_bwd.  The
 // caller keeps the BINNING buffer from being reused before the auxiliary stream is done with it
 // (gsr_forward_info.aux_stream: torch's record_stream on an ExternalStream of it).
+// Off by default (GSR_ITEMS_AUX=1 turns it on): with the item kernel's per-wave reservations it is
+// short, and on the auxiliary stream it cost the 3-stream headline step 4-5 % (an extra stream competing
+// for the chip, the cross-stream event per view).
 bool g_items_aux = [] {
     const char *e = getenv("GSR_ITEMS_AUX");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
 }();
 std::mutex g_items_mu;
 std::map<int, hipStream_t> g_aux;                       // device -> auxiliary stream
@@ -585,7 +589,7 @@ int async_redo(AsyncFwd &f, hipStream_t H) {
     HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)((char *)bin + bin_bytes + item_bytes), H));
     HIP_TRY(launch_render_fwd(a, H));
     if (GSR_FWD_ITEMS && f.prep)
-        HIP_TRY(launch_bwd_items_raw((int)K, f.T, a.P, a.ranges, a.tile_maxc, (uint2 *)((char *)bin + bin_bytes), H));
+        HIP_TRY(launch_bwd_items_raw((int)K, f.T, a.P, a.ranges, a.tile_maxc, (uint2 *)((char *)bin + bin_bytes), a.items_ws, H));
     HIP_TRY(hipStreamSynchronize(H));
     f.bin = bin;
     f.layout = (int)K;
@@ -768,7 +772,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
             hipStream_t used = nullptr;
             HIP_TRY(items_fork(dev, s, items, [&](hipStream_t q) {
                 Phase ph(q, "bwd_items");
-                return launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, q, sa.spec_ok);
+                return launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, q, sa.spec_ok);
             }, &used));
             info->aux_stream = used;
         }
@@ -842,7 +846,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         hipStream_t used = nullptr;
         HIP_TRY(items_fork(dev, s, items, [&](hipStream_t q) {
             Phase ph(q, "bwd_items");
-            return launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, q);
+            return launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, q);
         }, &used));
         if (used) info->aux_stream = used;
     }
@@ -1017,7 +1021,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.radii = radii;
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff; a.clampm = f.clampm;
     a.ranges = f.ranges; a.pix_end = f.pix_end; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
-    a.seg_off = f.seg_off; a.meta = f.meta;
+    a.seg_off = f.seg_off; a.meta = f.meta; a.items_ws = f.items_ws;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
     a.dL_dcolor = dL_dcolor;
     const ScratchLayout SL(num_rendered, a.gx * a.gy);

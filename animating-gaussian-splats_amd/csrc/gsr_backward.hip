@@ -79,6 +79,112 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
     }
 }
 
+// The same item list built over the whole chip (the single block above runs on ONE CU: ~30 us at C3,
+// 21 at C2, on the view's critical path).  k_items_count: one thread per tile counts its items per cost
+// bucket in an LDS histogram, the block adds its non-zero buckets into the workspace's global counts,
+// and the last block to finish (a done counter) turns the counts into the buckets' cursors (exclusive
+// scan, descending cost).  k_items_emit: each block counts its tiles' items again, reserves its run in
+// every bucket with one global atomic, and hands out the slots from LDS.  Order inside a bucket
+// follows the atomics (scheduling only).
+#ifndef GSR_ITEMS_MB
+#define GSR_ITEMS_MB 1  // 0: the single-block k_bwd_items
+#endif
+constexpr int kItemsBlock = 256;  // tiles (threads) per block
+struct ItemBucket {  // item cost -> LPT bucket (descending cost) for segments of 2^ks entries
+    uint32_t shift;
+    __device__ explicit ItemBucket(int ks) {
+        const uint32_t mx = (4u << ks) + kItemStartCost;
+        shift = mx >= (uint32_t)kOrderBuckets ? 32 - __builtin_clz(mx / kOrderBuckets) : 0;
+    }
+    __device__ uint32_t operator()(uint32_t cost) const {
+        return (uint32_t)kOrderBuckets - 1u - min(cost >> shift, (uint32_t)kOrderBuckets - 1u);
+    }
+};
+// f(item code, bucket) for every item of a tile with n list entries and quarter maxima mq
+template <typename F>
+__device__ inline void for_tile_items(uint32_t n, uint4 mq, int ks, const ItemBucket &bk, F f) {
+    const uint32_t J = bwd_item_count(n, mq, ks), Z = bwd_zero_items(n, mq);
+    for (uint32_t j = 0; j < J + Z; ++j) {
+        const uint32_t cost = j < J ? bwd_item_cost(j, mq, ks) + kItemStartCost : kItemStartCost;
+        f(j < J ? j : kZeroItem | (j - J), bk(cost));
+    }
+}
+
+__global__ __launch_bounds__(kItemsBlock) void k_items_count(int T, const uint2 *__restrict__ ranges,
+                                                             const uint32_t *__restrict__ tile_maxc,
+                                                             uint2 *__restrict__ items, uint32_t *__restrict__ ws,
+                                                             const uint32_t *__restrict__ spec_ok, int ks) {
+    __shared__ uint32_t s_hist[kOrderBuckets];
+    __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_last;
+    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
+    __syncthreads();
+    const ItemBucket bk(ks);
+    const int t = blockIdx.x * kItemsBlock + (int)threadIdx.x;
+    if (t < T) {
+        const uint2 rg = ranges[t];
+        const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[t];
+        for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t, uint32_t b) { atomicAdd(&s_hist[b], 1u); });
+    }
+    lds_barrier();  // (no-return LDS atomics)
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) {
+        const uint32_t h = s_hist[b];
+        if (h) atomicAdd(&ws[b], h);
+    }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&ws[2 * kOrderBuckets], 1u) == gridDim.x - 1 ? 1u : 0u;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    // the last block: every block's counts are in; cursors = exclusive scan, counts + counter reset
+    constexpr int kPer = kOrderBuckets / kItemsBlock;
+    const int b0 = (int)threadIdx.x * kPer;
+    uint32_t h[kPer], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        h[i] = __hip_atomic_load(&ws[b0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sum += h[i];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan_u32(sum, s_red, &tot);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        ws[kOrderBuckets + b0 + i] = ex;
+        ws[b0 + i] = 0;
+        ex += h[i];
+    }
+    if (threadIdx.x == 0) {
+        items[0] = make_uint2(tot, 0u);
+        ws[2 * kOrderBuckets] = 0;
+    }
+}
+
+__global__ __launch_bounds__(kItemsBlock) void k_items_emit(int T, const uint2 *__restrict__ ranges,
+                                                            const uint32_t *__restrict__ tile_maxc,
+                                                            uint2 *__restrict__ items, uint32_t *__restrict__ ws,
+                                                            const uint32_t *__restrict__ spec_ok, int ks) {
+    __shared__ uint32_t s_cur[kOrderBuckets];
+    if (spec_ok && *spec_ok == 0u) return;
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_cur[b] = 0;
+    __syncthreads();
+    const ItemBucket bk(ks);
+    const int t = blockIdx.x * kItemsBlock + (int)threadIdx.x;
+    const uint2 rg = t < T ? ranges[t] : make_uint2(0, 0);
+    const uint4 mq = t < T ? reinterpret_cast<const uint4 *>(tile_maxc)[t] : make_uint4(0, 0, 0, 0);
+    for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t, uint32_t b) { atomicAdd(&s_cur[b], 1u); });
+    lds_barrier();  // (no-return LDS atomics)
+    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) {  // this block's run in each bucket
+        const uint32_t h = s_cur[b];
+        if (h) s_cur[b] = atomicAdd(&ws[kOrderBuckets + b], h);
+    }
+    lds_barrier();
+    for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t code, uint32_t b) {
+        items[1 + atomicAdd(&s_cur[b], 1u)] = make_uint2((uint32_t)t, code);
+    });
+}
+
 // One wave64 per (tile, segment) item, 4 pixels per lane (pixel k of lane l: column l & 15, row
 // (l >> 4) + 4 k, i.e. quarter k = rows 4k..4k+3), reverse walk over the segment's entries in
 // batches of 64.  Per surviving (tile, Gaussian) pair each contributing pixel adds s = dL/dG * G
@@ -1210,13 +1316,19 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 
 // ==========================================================================================
 hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
-                                hipStream_t s, const uint32_t *spec_ok) {
+                                uint32_t *ws, hipStream_t s, const uint32_t *spec_ok) {
     if (K == 0) return hipSuccess;
-    k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items, spec_ok, seg_log2(P));
+    if (GSR_ITEMS_MB) {
+        const int nb = div_up(T, kItemsBlock);
+        k_items_count<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
+        k_items_emit<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
+    } else {
+        k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items, spec_ok, seg_log2(P));
+    }
     return hipGetLastError();
 }
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
-    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.P, a.ranges, a.tile_maxc, a.items, s);
+    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.P, a.ranges, a.tile_maxc, a.items, a.items_ws, s);
 }
 
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {

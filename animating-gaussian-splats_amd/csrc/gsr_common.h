@@ -130,13 +130,21 @@ __host__ __device__ inline size_t max_bwd_items(int K, int T) {
     return (k >> kSegLog2Min) + k / kZeroChunk + (k < (size_t)T ? k : (size_t)T) + 1;
 }
 
+// Cost buckets of the longest-first (LPT) dispatch orders (lpt_order, the backward's item list).
+constexpr int kOrderBuckets = 2048;
+// The backward item builder's workspace (k_items_count / k_items_emit, IMAGE.items_ws): per-bucket item
+// counts [0, kOrderBuckets), the buckets' cursors [kOrderBuckets, 2 kOrderBuckets), the builder's done
+// counter [2 kOrderBuckets].  k_bin_count zeroes it in every forward; the count kernel's last block
+// leaves the counts and the counter at zero again, so a second build (a repeated backward) starts clean.
+constexpr int kItemsWsWords = 2 * kOrderBuckets + 64;
+
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
 //   pix_end: per pixel (C0, C1, C2, T) at the end of the blend (accumulated colour without the
 //            background, final transmittance);  seg_off: per tile, exclusive prefix of its interior
 //            segment boundaries (seg_bounds) -> index of its first saved boundary state.
 struct ImageLayout {
     size_t ranges, pix_end, n_contrib, tile_maxc, tile_order_f, seg_off, sort_lists,
-        tile_count, tile_cursor, block_sums, block_off, meta, chunk_off, total;
+        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, chunk_off, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -154,6 +162,7 @@ struct ImageLayout {
         block_sums = o;  o = align256(o + sizeof(uint32_t) * (NB + 1));
         block_off = o;   o = align256(o + sizeof(uint32_t) * (NB + 1));
         meta = o;        o = align256(o + sizeof(uint32_t) * 16);
+        items_ws = o;    o = align256(o + sizeof(uint32_t) * kItemsWsWords);
         // (chunk, tile) counts, then each chunk's slab offset inside the tile's range (LDS binning)
         chunk_off = o;   o = align256(o + (T <= kMaxLdsTiles ? sizeof(uint32_t) * (size_t)NB * T : 0));
         total = o;
@@ -598,7 +607,6 @@ __device__ inline void wave_lds_sync() {
 // Longest-processing-time-first dispatch order, computed by ONE block: order[] lists the T tiles
 // by descending cost(t) (bucketed into 2048 log-free linear buckets; arbitrary order inside a bucket,
 // which only affects scheduling).  `s_hist` must hold 2048 words, `s_red` 16.  All threads call it.
-constexpr int kOrderBuckets = 2048;
 struct IdentityPos { __device__ uint32_t operator()(uint32_t p) const { return p; } };
 template <typename CostFn, typename PosMap = IdentityPos>
 __device__ inline void lpt_order(int T, CostFn cost, uint32_t *__restrict__ order, uint32_t *s_hist,

@@ -140,10 +140,13 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
                                                    const uint32_t *__restrict__ tiles,
                                                    uint32_t *__restrict__ tile_count,
                                                    uint32_t *__restrict__ block_sums,
-                                                   uint32_t *__restrict__ chunk_off) {
+                                                   uint32_t *__restrict__ chunk_off,
+                                                   uint32_t *__restrict__ items_ws) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_red[16];
     const int b = blockIdx.x;
+    if (b == 0)  // the backward item builder's workspace starts zeroed (kItemsWsWords)
+        for (int i = threadIdx.x; i < kItemsWsWords; i += blockDim.x) items_ws[i] = 0;
     const int g0 = b * CH, g1 = min(P, g0 + CH);
     if (USE_LDS) {
         for (int t = threadIdx.x; t < T; t += blockDim.x) s_hist[t] = 0;
@@ -938,10 +941,10 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     if (bg.NB == 0) return hipSuccess;  // (tile_count was zeroed by k_preprocess)
     if (T <= kMaxLdsTiles)
     {
-        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, a.chunk_off);
+        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, a.chunk_off, a.items_ws);
         k_bin_colscan<<<div_up(T, kColW), kColW * kColG, 0, s>>>(T, bg.NB, a.chunk_off, a.tile_count);
     } else
-        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, nullptr);
+        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, nullptr, a.items_ws);
     return hipGetLastError();
 }
 

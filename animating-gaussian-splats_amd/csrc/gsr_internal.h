@@ -18,6 +18,7 @@ struct FwdArgs {
     uint2 *ranges; float4 *pix_end; uint32_t *n_contrib; uint32_t *tile_maxc;
     uint32_t *tile_order_f; uint32_t *seg_off; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta; uint32_t *chunk_off;
+    uint32_t *items_ws;
     // binning
     uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
@@ -43,7 +44,7 @@ struct BwdArgs {
     // saved state
     const float4 *rec; const uint2 *rect; const uint8_t *clampm;
     const uint32_t *goff; const uint2 *ranges; const float4 *pix_end; const uint32_t *n_contrib;
-    const uint32_t *tile_maxc; const uint32_t *seg_off; const uint32_t *meta;
+    const uint32_t *tile_maxc; const uint32_t *seg_off; const uint32_t *meta; uint32_t *items_ws;
     const uint32_t *point_list; const uint32_t *slot_emit; const float4 *seg_state;
     uint2 *items; uint32_t max_items;
     // scratch
@@ -69,7 +70,7 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
 
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s);
 hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
-                                hipStream_t s, const uint32_t *spec_ok = nullptr);
+                                uint32_t *ws, hipStream_t s, const uint32_t *spec_ok = nullptr);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 // Each Gaussian's per-pair records of one view summed in emission order into kPartial x P SoA sums
