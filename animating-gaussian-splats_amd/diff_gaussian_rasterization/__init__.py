@@ -24,7 +24,7 @@ from torch.autograd.graph import get_gradient_edge
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "set_async_forward",
+           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "set_async_forward", "async_forward",
            "pending_views", "clear_pending"]
 
 
@@ -154,8 +154,13 @@ _defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0",
           # gsr_forward_info_call): the stream does not idle while the host reads K and launches
           "speculate": os.environ.get("GSR_SPECULATE", "1") != "0",
           # forwards with a pair-count history return without reading num_rendered back
-          # (gsr_forward_async): one host thread keeps queueing views while the GPU renders
-          "async": os.environ.get("GSR_ASYNC_FORWARD", "1") != "0"}
+          # (gsr_forward_async): one host thread keeps queueing views on several streams while the
+          # GPU renders.  Off by default: on one stream (train.py's shape) and with one submitting
+          # thread per stream (the headline) the host wait for K is already hidden, and the asynchronous
+          # bookkeeping cost 1-3 % there; ``async_forward(True)`` / the env switch turn
+          # it on for one-thread multi-stream submission (splat_step.RenderStep does)
+          "async": os.environ.get("GSR_ASYNC_FORWARD", "0") == "1"}
+_async_tls = threading.local()  # async_forward(): a per-thread override of _defer["async"]
 _pending_lock = threading.Lock()
 _pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
 _queued = set()  # graph tasks whose flush callback is queued
@@ -183,6 +188,28 @@ def set_async_forward(on: bool) -> bool:
     prev = _defer["async"]
     _defer["async"] = bool(on)
     return prev
+
+
+class async_forward:
+    """Context manager: the asynchronous forward on (or off) for the calls this thread makes inside it,
+    whatever the process-wide setting (set_async_forward)."""
+
+    def __init__(self, on: bool = True):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.prev = getattr(_async_tls, "on", None)
+        _async_tls.on = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _async_tls.on = self.prev
+        return False
+
+
+def _async_on():
+    o = getattr(_async_tls, "on", None)
+    return _defer["async"] if o is None else o
 
 
 def _buffer_ptrs(alloc):
@@ -374,8 +401,12 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
 # Gradients made on L and read on C are record_stream'ed on C; leaf gradients are added into .grad in
 # place on L, and the end of the pass makes C wait for every L it used.  Results are bitwise those of
 # one stream: every gradient write is ordered (ordered_grad_write) and each consumer waits for its
-# producer.
-_VIEW_STREAMS = {"on": os.environ.get("GSR_VIEW_STREAMS", "1") != "0", "n": 3, "pool": {}, "next": {}}
+# producer.  Off by default (GSR_VIEW_STREAMS=1 / set_view_streams(True) turn it on): measured on the
+# unchanged train.py step the views' kernels overlap but the step does not get shorter -- the render
+# kernels are VALU-bound and slow each other down when they share the chip, and the hand-off adds host
+# time -- 1014-1031 Msplats/s without, 955-970 with.
+_VIEW_STREAMS = {"on": os.environ.get("GSR_VIEW_STREAMS", "0") == "1", "n": int(os.environ.get("GSR_VIEW_STREAMS_N", "3")),
+                 "pool": {}, "next": {}}
 
 
 def set_view_streams(on: bool) -> bool:
@@ -521,7 +552,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         # prepares it
         ctx.prep = bool(grad_mode) and any(ctx.needs_input_grad)
         fi, color, radii, depth, alloc, pending = _C._forward(
-            *args, 0, ctx.prep, _defer["speculate"], _defer["async"])
+            *args, 0, ctx.prep, _defer["speculate"], _async_on())
         ctx.raster_settings = rs
         ctx.num_rendered = fi.num_rendered
         ctx.binning_layout = fi.binning_layout
@@ -651,7 +682,7 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         fi, color, radii, depth, alloc, pending = _C._forward(
             rs.bg, means, colors, opacity_logits, log_scales, quaternions, rs.scale_modifier, empty,
             rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height, rs.image_width, sh,
-            rs.sh_degree, rs.campos, rs.prefiltered, _C.ACT_ALL, ctx.prep, _defer["speculate"], _defer["async"])
+            rs.sh_degree, rs.campos, rs.prefiltered, _C.ACT_ALL, ctx.prep, _defer["speculate"], _async_on())
         ctx.raster_settings = rs
         ctx.num_rendered = fi.num_rendered
         ctx.binning_layout = fi.binning_layout

@@ -11,7 +11,10 @@ drop-in ``GaussianRasterizer`` for the benchmark and the parity tests alike:
   stream further every call, so with 5 views on 3 streams the streams carry 2, 2, 1 views in turn
   instead of the first two always carrying two (their serial kernel chains bound the step);
 * ``threads``: one host thread per stream submits that stream's forwards, so a forward waiting for
-  its ``num_rendered`` read-back (the reference's host sync) blocks only its own stream;
+  its ``num_rendered`` read-back (the reference's host sync) blocks only its own stream; without
+  threads (one host thread for several streams) the forwards are asynchronous
+  (``diff_gaussian_rasterization.async_forward``: no host wait for the pair count), so that one thread
+  keeps every stream fed;
 * ``summed``: the views' images are backpropagated together (``torch.autograd.backward`` of all
   images with the fixed upstream gradient = the summed loss), so the deferred multi-view
   per-Gaussian pass covers every view when the inputs are leaves; ``per_view``: one backward per
@@ -26,11 +29,12 @@ from __future__ import annotations
 
 import os
 from concurrent.futures import ThreadPoolExecutor
+from contextlib import nullcontext as _nullcontext
 from typing import Callable, Sequence
 
 import torch
 
-from diff_gaussian_rasterization import GaussianRasterizer
+from diff_gaussian_rasterization import GaussianRasterizer, async_forward
 
 
 class RenderStep:
@@ -71,6 +75,10 @@ class RenderStep:
         off = self.calls % ns if self.rotate else 0  # stream of this call's first view
         self.calls += 1
         streams = self.streams[off:ns] + self.streams[:off] if ns > 1 else self.streams[:1]
+        with async_forward(True) if pool is None and ns > 1 else _nullcontext():
+            return self._run(views, ns, pool, streams)
+
+    def _run(self, views, ns, pool, streams):
         if self.shape == "summed":
             if pool is not None:
                 futs = [pool.submit(self._forwards, views[k::ns], streams[k]) for k in range(min(ns, len(views)))]
