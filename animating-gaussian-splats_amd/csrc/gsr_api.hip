@@ -236,6 +236,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.block_sums = (uint32_t *)(base + L.block_sums); a.block_off = (uint32_t *)(base + L.block_off);
     a.meta = (uint32_t *)(base + L.meta); a.chunk_off = (uint32_t *)(base + L.chunk_off);
     a.items_ws = (uint32_t *)(base + L.items_ws);
+    a.scan_ws = (uint32_t *)(base + L.scan_ws); a.tile_rank = (uint32_t *)(base + L.tile_rank);
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K, a.P);

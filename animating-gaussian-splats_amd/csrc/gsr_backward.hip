@@ -132,12 +132,13 @@ __global__ __launch_bounds__(kItemsBlock) void k_items_count(int T, const uint2 
         const uint32_t h = s_hist[b];
         if (h) atomicAdd(&ws[b], h);
     }
-    __threadfence();
+    // (no agent-scope fence: it would write back / invalidate the XCD's whole L2; the counts are
+    // device-scope atomics, drained by the workgroup-scope fence's vmcnt wait)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) s_last = atomicAdd(&ws[2 * kOrderBuckets], 1u) == gridDim.x - 1 ? 1u : 0u;
     __syncthreads();
     if (!s_last) return;
-    __threadfence();
     // the last block: every block's counts are in; cursors = exclusive scan, counts + counter reset
     constexpr int kPer = kOrderBuckets / kItemsBlock;
     const int b0 = (int)threadIdx.x * kPer;

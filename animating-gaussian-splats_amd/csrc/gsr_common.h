@@ -138,13 +138,33 @@ constexpr int kOrderBuckets = 2048;
 // leaves the counts and the counter at zero again, so a second build (a repeated backward) starts clean.
 constexpr int kItemsWsWords = 2 * kOrderBuckets + 64;
 
+// The single-pass tile scan of k_bin_colscan (IMAGE.scan_ws, zeroed by k_bin_count): one look-back
+// word per block of tiles (u64: flag in bits 62-63 -- kScanAgg: the block's own sums, kScanInc: the sums
+// of every block up to it -- pair count in bits 0-31, segment-boundary count in bits 32-61), then
+// counters (kScanCtr words: [0] block ticket, [1] done blocks, [2] mid lists, [3] long lists, [4] the
+// longest list), then the forward dispatch order's bucket counts (-> offsets, kOrderBuckets words).
+constexpr uint64_t kScanAgg = 1ull << 62, kScanInc = 2ull << 62;
+constexpr int kScanBlocksMax = 512;  // blocks of the LDS-binning column scan (T <= kMaxLdsTiles)
+constexpr int kScanCtr = 16;
+constexpr int kScanWsWords = 2 * kScanBlocksMax + kScanCtr + kOrderBuckets;
+// the forward's LPT dispatch bucket of a tile with c list entries (0 = longest): exact below 1024, then
+// 32 buckets per power of two (a fixed map, so the tiles can be bucketed before the longest is known)
+__host__ __device__ inline uint32_t lpt_bucket(uint32_t c) {
+    uint32_t b = c;
+    if (c >= 1024u) {
+        const uint32_t e = 31u - (uint32_t)__builtin_clz(c);
+        b = 1024u + ((e - 10u) << 5) + ((c >> (e - 5u)) & 31u);
+    }
+    return (uint32_t)kOrderBuckets - 1u - b;
+}
+
 // IMAGE (per pixel / per tile): tile ranges, blend state saved for backward, binning counters.
 //   pix_end: per pixel (C0, C1, C2, T) at the end of the blend (accumulated colour without the
 //            background, final transmittance);  seg_off: per tile, exclusive prefix of its interior
 //            segment boundaries (seg_bounds) -> index of its first saved boundary state.
 struct ImageLayout {
     size_t ranges, pix_end, n_contrib, tile_maxc, tile_order_f, seg_off, sort_lists,
-        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, chunk_off, total;
+        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, scan_ws, tile_rank, chunk_off, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -163,6 +183,8 @@ struct ImageLayout {
         block_off = o;   o = align256(o + sizeof(uint32_t) * (NB + 1));
         meta = o;        o = align256(o + sizeof(uint32_t) * 16);
         items_ws = o;    o = align256(o + sizeof(uint32_t) * kItemsWsWords);
+        scan_ws = o;     o = align256(o + sizeof(uint32_t) * kScanWsWords);
+        tile_rank = o;   o = align256(o + sizeof(uint32_t) * T);           // rank inside its LPT bucket
         // (chunk, tile) counts, then each chunk's slab offset inside the tile's range (LDS binning)
         chunk_off = o;   o = align256(o + (T <= kMaxLdsTiles ? sizeof(uint32_t) * (size_t)NB * T : 0));
         total = o;

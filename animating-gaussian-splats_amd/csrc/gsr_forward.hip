@@ -141,12 +141,16 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
                                                    uint32_t *__restrict__ tile_count,
                                                    uint32_t *__restrict__ block_sums,
                                                    uint32_t *__restrict__ chunk_off,
-                                                   uint32_t *__restrict__ items_ws) {
+                                                   uint32_t *__restrict__ items_ws,
+                                                   uint32_t *__restrict__ scan_ws) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_hist[];
     __shared__ uint32_t s_red[16];
     const int b = blockIdx.x;
-    if (b == 0)  // the backward item builder's workspace starts zeroed (kItemsWsWords)
+    if (b == 0) {  // the tile scan's and the backward item builder's workspaces start zeroed
         for (int i = threadIdx.x; i < kItemsWsWords; i += blockDim.x) items_ws[i] = 0;
+        if (scan_ws)
+            for (int i = threadIdx.x; i < kScanWsWords; i += blockDim.x) scan_ws[i] = 0;
+    }
     const int g0 = b * CH, g1 = min(P, g0 + CH);
     if (USE_LDS) {
         for (int t = threadIdx.x; t < T; t += blockDim.x) s_hist[t] = 0;
@@ -181,24 +185,63 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
 // (at most kColR) counts in registers between the two passes, so the matrix is read once.  Replaces
 // one device-scope atomic per non-empty (chunk, tile) bin in k_bin_count and a returning one in
 // k_bin_emit (~2 M each at C3) with 2 x NB x T x 4 bytes of coalesced traffic.
+//
+// The same kernel then finishes the tile scan in a single pass (what a separate one-block scan kernel
+// did, ~25 us at C3 on ONE CU): blocks take their tile columns by ticket (dispatch order), publish their
+// columns' pair and segment-boundary sums and look back over the earlier blocks' words (decoupled
+// look-back: one wave reads 64 predecessors at a time) for their exclusive prefix, then write their
+// tiles' ranges, cursors, segment offsets, list classes and LPT bucket ranks.  The last block to finish
+// (done counter) turns the LPT bucket counts into offsets (k_bin_emit scatters the dispatch order),
+// scans the chunk sums into chunk emission offsets and publishes K and the list classes to meta and
+// the host words -- as k_bin_scan does.
 #ifndef GSR_COLSCAN_W
 #define GSR_COLSCAN_W 32  // tile columns per k_bin_colscan block (32 x kColG threads)
 #endif
 constexpr int kColW = GSR_COLSCAN_W, kColG = 32, kColR = 16;
 static_assert(kColG * kColR >= 512, "BinGrid makes at most 512 chunks");
-__global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(int T, int NB, uint32_t *__restrict__ chunk_off,
-                                                      uint32_t *__restrict__ tile_count) {
+static_assert(kColW <= 64 && kMaxLdsTiles <= kColW * kScanBlocksMax, "look-back: one wave per block, <= kScanBlocksMax blocks");
+// Slab order inside a tile's range: the chunks that k_bin_emit runs on one XCD (blocks go round-robin
+// over the 8 XCDs: chunk b on XCD b % 8) are adjacent, so each XCD's scattered 16-byte pair stores
+// into a tile fill one contiguous run and the partial cache lines merge in that XCD's L2 instead of
+// being written back from up to 8 of them (pair writes were billed 2x their bytes).  The order inside
+// a tile is made canonical by the tile sort, so only placement changes.
+#ifndef GSR_XCD_SLABS
+#define GSR_XCD_SLABS 1
+#endif
+__device__ inline int slab_chunk(int k, int NB) {  // the chunk at slab position k of a tile's range
+    if (!GSR_XCD_SLABS) return k;
+    const int q = NB >> 3, r = NB & 7, big = r * (q + 1);
+    int x, i;
+    if (k < big) { x = k / (q + 1); i = k - x * (q + 1); }
+    else { const int k2 = k - big; x = r + k2 / q; i = k2 - (x - r) * q; }
+    return i * 8 + x;
+}
+__global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
+    int T, int NB, uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ tile_count, uint2 *__restrict__ ranges,
+    uint32_t *__restrict__ tile_cursor, uint32_t *__restrict__ seg_off, uint32_t *__restrict__ sort_lists,
+    uint32_t *__restrict__ tile_rank, uint32_t *__restrict__ ws, const uint32_t *__restrict__ block_sums,
+    uint32_t *__restrict__ block_off, uint32_t *__restrict__ meta, uint32_t *host_words, uint32_t cap, int ks) {
     __shared__ uint32_t s_part[kColG][kColW + 1];
+    __shared__ uint32_t s_tile[kColW];
+    __shared__ uint32_t s_blk, s_last;
+    __shared__ uint32_t s_red[16];
+    __shared__ uint32_t s_lpt[kOrderBuckets];  // this block's tiles per LPT bucket, then the block's base
+    uint64_t *look = reinterpret_cast<uint64_t *>(ws);
+    uint32_t *ctr = ws + 2 * kScanBlocksMax, *lpt = ctr + kScanCtr;
+    if (threadIdx.x == 0) s_blk = atomicAdd(&ctr[0], 1u);  // blocks take column ranges in dispatch order
+    for (int i = threadIdx.x; i < kOrderBuckets; i += blockDim.x) s_lpt[i] = 0;
+    __syncthreads();
+    const int blk = (int)s_blk;
     const int col = threadIdx.x % kColW, grp = threadIdx.x / kColW;
-    const int t = blockIdx.x * kColW + col;
+    const int t = blk * kColW + col;
     const int R = div_up(NB, kColG);
     const int r0 = min(NB, grp * R), r1 = min(NB, r0 + R);
     uint32_t *p = chunk_off + t;
     uint32_t v[kColR];
     uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kColR; ++k) {
-        v[k] = (t < T && r0 + k < r1) ? p[(size_t)(r0 + k) * T] : 0u;
+    for (int k = 0; k < kColR; ++k) {  // slab positions r0 .. r1 - 1 of this group
+        v[k] = (t < T && r0 + k < r1) ? p[(size_t)slab_chunk(r0 + k, NB) * T] : 0u;
         sum += v[k];
     }
     s_part[grp][col] = sum;
@@ -210,12 +253,122 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(int T, int NB, ui
         pre += k < grp ? c : 0u;
         tot += c;
     }
-    if (t >= T) return;
-    if (grp == 0) tile_count[t] = tot;
+    if (t < T) {
+        if (grp == 0) tile_count[t] = tot;
 #pragma unroll
-    for (int k = 0; k < kColR; ++k) {
-        if (r0 + k < r1) p[(size_t)(r0 + k) * T] = pre;
-        pre += v[k];
+        for (int k = 0; k < kColR; ++k) {
+            if (r0 + k < r1) p[(size_t)slab_chunk(r0 + k, NB) * T] = pre;
+            pre += v[k];
+        }
+    }
+    if (grp == 0) s_tile[col] = t < T ? tot : 0u;
+    __syncthreads();
+    if (threadIdx.x < 64) {  // wave 0: the block's prefix, then its tiles' outputs
+        const int lane = threadIdx.x;
+        const uint32_t cnt = lane < kColW ? s_tile[lane] : 0u, sb = seg_bounds(cnt, ks);
+        const uint32_t ic = wave_incl_scan_u32(cnt), is = wave_incl_scan_u32(sb);
+        const uint32_t agg_c = (uint32_t)__builtin_amdgcn_readlane((int)ic, 63);
+        const uint32_t agg_s = (uint32_t)__builtin_amdgcn_readlane((int)is, 63);
+        if (lane == 0)
+            __hip_atomic_store(&look[blk], (blk == 0 ? kScanInc : kScanAgg) | ((uint64_t)agg_s << 32) | agg_c,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t ex_c = 0, ex_s = 0;
+        for (int base = blk - 1; base >= 0; base -= 64) {  // predecessors base, base - 1, ... (lane order)
+            const int j = base - lane;
+            uint64_t w;
+            uint64_t inc, zero;
+            for (;;) {
+                w = j >= 0 ? __hip_atomic_load(&look[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kScanInc;
+                inc = __ballot((w >> 62) == 2u);
+                zero = __ballot((w >> 62) == 0u);
+                const uint64_t upto = inc ? (~0ull >> (63 - __builtin_ctzll(inc))) : ~0ull;  // lanes up to the nearest inclusive
+                if (!(zero & upto)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const int first = inc ? __builtin_ctzll(inc) : 64;
+            const uint32_t wc = lane <= first ? (uint32_t)w : 0u;
+            const uint32_t ws_ = lane <= first ? (uint32_t)(w >> 32) & 0x3FFFFFFFu : 0u;
+            ex_c += (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(wc), 63);
+            ex_s += (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(ws_), 63);
+            if (inc) break;
+        }
+        if (lane == 0 && blk > 0)
+            __hip_atomic_store(&look[blk], kScanInc | ((uint64_t)(ex_s + agg_s) << 32) | (ex_c + agg_c),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int tl = blk * kColW + lane;
+        // rank inside the tile's LPT bucket: the block's tiles of one bucket take one global reservation
+        // (same-address global atomics serialise: one per tile cost ~100 us at C3)
+        const uint32_t bkt = lpt_bucket(cnt);
+        const bool mine = lane < kColW && tl < T;
+        const uint32_t local = mine ? atomicAdd(&s_lpt[bkt], 1u) : 0u;
+        wave_lds_sync();
+        if (mine && local == 0) s_lpt[bkt] = atomicAdd(&lpt[bkt], s_lpt[bkt]);
+        wave_lds_sync();
+        if (mine) tile_rank[tl] = s_lpt[bkt] + local;
+        if (mine) {
+            const uint32_t ex = ex_c + ic - cnt;
+            ranges[tl] = cnt ? make_uint2(ex, ex + cnt) : make_uint2(0, 0);  // empty: {0,0} like the reference
+            tile_cursor[tl] = ex;
+            seg_off[tl] = ex_s + is - sb;
+            if (cnt > (uint32_t)kSortCap) {  // long: merge-sorted; listed from the end
+                sort_lists[T - 1 - atomicAdd(&ctr[3], 1u)] = (uint32_t)tl;
+                atomicMax(&ctr[4], cnt);
+            } else if (cnt > (uint32_t)kFwdSortCap) {
+                sort_lists[atomicAdd(&ctr[2], 1u)] = (uint32_t)tl;
+            }
+        }
+    }
+    // No agent-scope fences: the 8 XCDs' L2s are not coherent, so such a fence writes back / invalidates
+    // the whole L2 (a first version with __threadfence() and acquire / release look-back words took
+    // ~100 us).  Everything another block reads here is a device-scope atomic (payload and flag share
+    // one word); the wave drains its own atomics (workgroup-scope fence: a vmcnt wait) before the block
+    // counts itself done.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0) s_last = atomicAdd(&ctr[1], 1u) == gridDim.x - 1 ? 1u : 0u;
+    __syncthreads();
+    if (!s_last) return;
+    // the last block: every tile is classified and ranked
+    const uint64_t fin = __hip_atomic_load(&look[gridDim.x - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t K = (uint32_t)fin, n_seg = (uint32_t)(fin >> 32) & 0x3FFFFFFFu;
+    {   // LPT bucket counts -> offsets (kOrderBuckets / blockDim.x per thread)
+        constexpr int kPer = kOrderBuckets / (kColW * kColG);
+        uint32_t h[kPer], hs = 0;
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            h[i] = __hip_atomic_load(&lpt[threadIdx.x * kPer + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hs += h[i];
+        }
+        uint32_t tt;
+        uint32_t e = block_excl_scan_u32(hs, s_red, &tt);
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) {
+            lpt[threadIdx.x * kPer + i] = e;
+            e += h[i];
+        }
+    }
+    {   // chunk emission offsets (NB <= 512 <= blockDim.x)
+        const uint32_t bs = (int)threadIdx.x < NB ? block_sums[threadIdx.x] : 0u;
+        uint32_t btot;
+        const uint32_t bex = block_excl_scan_u32(bs, s_red, &btot);
+        if ((int)threadIdx.x < NB) block_off[threadIdx.x] = bex;
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t n_mid = __hip_atomic_load(&ctr[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t n_long = __hip_atomic_load(&ctr[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t max_long = __hip_atomic_load(&ctr[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        seg_off[T] = n_seg;
+        meta[0] = K;
+        // speculative enqueue (gsr_forward_info): the kernels queued before the host read K run
+        // only when the BINNING capacity holds K and no list needs the merge sort
+        meta[1] = (cap && K <= cap && n_long == 0u) ? 1u : 0u;
+        meta[2] = n_mid;
+        if (host_words) {
+            __hip_atomic_store(host_words + 1, n_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_words + 2, n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_words + 3, max_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(host_words, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -372,12 +525,21 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_emit(int P, int CH, int T, 
                                                   uint32_t *__restrict__ goff,
                                                   uint4 *__restrict__ pairs, uint32_t K,
                                                   const uint32_t *__restrict__ chunk_off,
-                                                  const uint32_t *__restrict__ spec_ok) {
+                                                  const uint32_t *__restrict__ spec_ok,
+                                                  const uint32_t *__restrict__ tile_count,
+                                                  const uint32_t *__restrict__ tile_rank,
+                                                  const uint32_t *__restrict__ lpt_off,
+                                                  uint32_t *__restrict__ tile_order) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_cur[];
     __shared__ uint32_t s_red[16];
     if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: the host redoes it
     const int b = blockIdx.x;
     const int g0 = b * CH, g1 = min(P, g0 + CH);
+    if (tile_rank) {  // the forward's dispatch order (k_bin_colscan's LPT buckets): this block's share of tiles
+        const int per = div_up(T, (int)gridDim.x), t1 = min(T, (b + 1) * per);
+        for (int t = b * per + (int)threadIdx.x; t < t1; t += blockDim.x)
+            tile_order[lpt_off[lpt_bucket(tile_count[t])] + tile_rank[t]] = (uint32_t)t;
+    }
     GSR_EMIT_STAMP(0);
     if (USE_LDS) {  // this chunk's slab in every tile: the tile's range start + the column scan
         const uint32_t *row = chunk_off + (size_t)b * T;
@@ -731,6 +893,11 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const int n = (int)(rg.y - rg.x);
     const bool sorted_here = n <= kFwdSortCap;
     if (n > 0 && sorted_here) {
+#ifdef GSR_FWD_NOSORT  // timing experiment only (wrong order): the share of the in-render sort
+        for (int i = threadIdx.x; i < n; i += 256) { const uint4 q = pairs[rg.x + i]; s_key[i] = pair_key(q); s_u.val[i] = q.z; }
+        __syncthreads();
+        if (false)
+#endif
         if (n <= 256) block_sort_tile<1, 4>(n, rg.x, pairs, s_key, s_u.val);
         else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, pairs, s_key, s_u.val);
         else block_sort_tile<4, 4>(n, rg.x, pairs, s_key, s_u.val);
@@ -940,19 +1107,26 @@ hipError_t launch_bin_count(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;  // (tile_count was zeroed by k_preprocess)
     if (T <= kMaxLdsTiles)
-    {
-        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, a.chunk_off, a.items_ws);
-        k_bin_colscan<<<div_up(T, kColW), kColW * kColG, 0, s>>>(T, bg.NB, a.chunk_off, a.tile_count);
-    } else
-        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, nullptr, a.items_ws);
+        k_bin_count<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, a.chunk_off, a.items_ws, a.scan_ws);
+    else
+        k_bin_count<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.tile_count, a.block_sums, nullptr, a.items_ws, nullptr);
     return hipGetLastError();
 }
 
+// LDS binning (T <= kMaxLdsTiles): the column scan with the single-pass tile scan; otherwise the
+// one-block scan over the globally counted tiles
 hipError_t launch_bin_scan(const FwdArgs &a, uint32_t *host_words, hipStream_t s) {
     const BinGrid bg(a.P);
-    k_bin_scan<<<1, 1024, 0, s>>>(a.gx * a.gy, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
-                                  a.block_sums, a.block_off, a.meta, host_words, a.tile_order_f,
-                                  a.sort_lists, a.seg_off, a.spec_cap, seg_log2(a.P));
+    const int T = a.gx * a.gy;
+    if (T <= kMaxLdsTiles && bg.NB > 0)
+        k_bin_colscan<<<div_up(T, kColW), kColW * kColG, 0, s>>>(T, bg.NB, a.chunk_off, a.tile_count, a.ranges,
+                                                                a.tile_cursor, a.seg_off, a.sort_lists, a.tile_rank,
+                                                                a.scan_ws, a.block_sums, a.block_off, a.meta,
+                                                                host_words, a.spec_cap, seg_log2(a.P));
+    else
+        k_bin_scan<<<1, 1024, 0, s>>>(T, bg.NB, a.tile_count, a.ranges, a.tile_cursor,
+                                      a.block_sums, a.block_off, a.meta, host_words, a.tile_order_f,
+                                      a.sort_lists, a.seg_off, a.spec_cap, seg_log2(a.P));
     return hipGetLastError();
 }
 
@@ -961,9 +1135,11 @@ hipError_t launch_bin_emit(const FwdArgs &a, int K, hipStream_t s) {
     const int T = a.gx * a.gy;
     if (bg.NB == 0) return hipSuccess;
     if (T <= kMaxLdsTiles)
-        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off, a.spec_ok);
+        k_bin_emit<true><<<bg.NB, kBinThreads, sizeof(uint32_t) * T, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off, a.spec_ok,
+                                                                           a.tile_count, a.tile_rank, a.scan_ws + 2 * kScanBlocksMax + kScanCtr, a.tile_order_f);
     else
-        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off, a.spec_ok);
+        k_bin_emit<false><<<bg.NB, kBinThreads, 0, s>>>(a.P, bg.CH, T, a.gx, a.rect, a.tiles, a.depth, a.block_off, a.tile_cursor, a.goff, a.pairs, (uint32_t)K, a.chunk_off, a.spec_ok,
+                                                        nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError();
 }
 

@@ -18,7 +18,7 @@ struct FwdArgs {
     uint2 *ranges; float4 *pix_end; uint32_t *n_contrib; uint32_t *tile_maxc;
     uint32_t *tile_order_f; uint32_t *seg_off; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta; uint32_t *chunk_off;
-    uint32_t *items_ws;
+    uint32_t *items_ws; uint32_t *scan_ws; uint32_t *tile_rank;
     // binning
     uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
