@@ -228,7 +228,11 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
     __shared__ uint32_t s_lpt[kOrderBuckets];  // this block's tiles per LPT bucket, then the block's base
     uint64_t *look = reinterpret_cast<uint64_t *>(ws);
     uint32_t *ctr = ws + 2 * kScanBlocksMax, *lpt = ctr + kScanCtr;
-    if (threadIdx.x == 0) s_blk = atomicAdd(&ctr[0], 1u);  // blocks take column ranges in dispatch order
+#ifndef GSR_SCAN_TICKET
+#define GSR_SCAN_TICKET 0  // 1: blocks take their columns by an atomic ticket (0: blockIdx -- a grid is
+                           // dispatched in block order, so every block a look-back waits on is resident)
+#endif
+    if (threadIdx.x == 0) s_blk = GSR_SCAN_TICKET ? atomicAdd(&ctr[0], 1u) : blockIdx.x;
     for (int i = threadIdx.x; i < kOrderBuckets; i += blockDim.x) s_lpt[i] = 0;
     __syncthreads();
     const int blk = (int)s_blk;
@@ -367,7 +371,11 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
             __hip_atomic_store(host_words + 1, n_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_words + 2, n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_words + 3, max_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#ifdef GSR_SCAN_NO_RELEASE  // timing experiment only: the cost of the system-scope release (L2 write-back)
+            __hip_atomic_store(host_words, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
             __hip_atomic_store(host_words, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
         }
     }
 }
