@@ -371,11 +371,7 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
             __hip_atomic_store(host_words + 1, n_mid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_words + 2, n_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(host_words + 3, max_long, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#ifdef GSR_SCAN_NO_RELEASE  // timing experiment only: the cost of the system-scope release (L2 write-back)
-            __hip_atomic_store(host_words, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
             __hip_atomic_store(host_words, K, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#endif
         }
     }
 }

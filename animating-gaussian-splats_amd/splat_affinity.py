@@ -1,0 +1,108 @@
+"""Host-thread placement for one GPU's process (what a launcher's numactl / taskset would do).
+
+The render step submits many small kernels from one or a few host threads (C2: ~50 launches per
+step at ~0.2 ms of GPU work per view), so its throughput follows the host threads' cores.  On the
+shared GPU boxes every process may run on all 256 CPUs of the host (two NUMA nodes) under a cgroup
+quota, and the kernel scheduler moves the submitting threads onto cores that other tenants keep busy:
+C2 ran at 255-460 Msplats/s from one process to the next on one box, and at 479-487 with the process
+pinned to a few idle CPUs of one node (tools/c2_pin.py).  ``pin_host_threads`` picks such CPUs -- the
+least busy ones (sampled from /proc/stat) of the GPU's NUMA node, in this local rank's share of the
+node when several ranks share it -- and pins every thread of the process to them, including the HIP
+runtime's and the library's resolver thread.  Nothing on the device side changes.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+
+def _cpulist(text):
+    out = []
+    for part in text.strip().split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _gpu_numa_node(dev_index):
+    """NUMA node of the visible GPU ``dev_index`` (-1 when unknown), from its PCI address."""
+    try:
+        import torch
+        pr = torch.cuda.get_device_properties(dev_index)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        return int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+    except (AttributeError, OSError, ValueError, RuntimeError):
+        return -1
+
+
+def _busy_fraction(cpus, interval=0.05):
+    """Busy fraction of each CPU over ``interval`` seconds (/proc/stat), {} when unavailable."""
+    def sample():
+        out = {}
+        try:
+            for line in open("/proc/stat"):
+                if line.startswith("cpu") and line[3].isdigit():
+                    f = line.split()
+                    v = [int(x) for x in f[1:]]
+                    idle = v[3] + (v[4] if len(v) > 4 else 0)
+                    out[int(f[0][3:])] = (sum(v), idle)
+        except OSError:
+            pass
+        return out
+    a = sample()
+    time.sleep(interval)
+    b = sample()
+    busy = {}
+    for c in cpus:
+        if c in a and c in b:
+            tot, idle = b[c][0] - a[c][0], b[c][1] - a[c][1]
+            busy[c] = 1.0 - idle / tot if tot > 0 else 0.0
+    return busy
+
+
+def choose_cpus(dev_index=0, local_rank=0, local_world=1, n=8):
+    """The CPUs ``pin_host_threads`` would use (sorted), or [] when there is no choice to make."""
+    if n <= 0 or not hasattr(os, "sched_getaffinity"):
+        return []
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) <= n:
+        return []
+    node = _gpu_numa_node(dev_index)
+    pool = allowed
+    if node >= 0:
+        try:
+            local = [c for c in _cpulist(open(f"/sys/devices/system/node/node{node}/cpulist").read()) if c in allowed]
+            pool = local if len(local) >= n else allowed
+        except OSError:
+            pass
+    if local_world > 1:  # this rank's contiguous share of the pool (ranks of one node do not collide)
+        per = max(n, len(pool) // local_world)
+        start = (local_rank * per) % max(len(pool), 1)
+        share = pool[start:start + per]
+        pool = share if len(share) >= n else pool
+    busy = _busy_fraction(pool)
+    return sorted(sorted(pool, key=lambda c: (busy.get(c, 1.0), c))[:n])
+
+
+def pin_host_threads(dev_index=0, local_rank=0, local_world=1, n=8):
+    """Pin every thread of this process to ``choose_cpus(...)``; returns the CPUs (or [] when unpinned).
+    Call it once the GPU is initialised (so the runtime's threads exist and get pinned too)."""
+    cpus = choose_cpus(dev_index, local_rank, local_world, n)
+    if not cpus:
+        return []
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), cpus)
+        except OSError:
+            pass
+    return cpus
+
+
+def unpin_host_threads(cpus):
+    """Give every thread of the process the CPU set ``cpus`` (e.g. the affinity before pinning)."""
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), cpus)
+        except OSError:
+            pass

@@ -712,6 +712,11 @@ def main():
                          "rehearse the multi-rank path on one GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / sharding / collective (gloo, no GPU work)")
+    ap.add_argument("--pin-cpus", type=int, default=int(os.environ.get("GSR_PIN_CPUS", "8")),
+                    help="pin the process's threads to this many of the least busy CPUs of the GPU's NUMA "
+                         "node (this rank's share of it) once the GPU is up -- a launcher's numactl; the "
+                         "submitting threads otherwise wander over the shared host's 256 CPUs (0 = off; "
+                         "splat_affinity.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="OpenMP threads of the CPU baseline (0 = every CPU this process may run on, "
@@ -784,6 +789,13 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     _C.load_library()
+    torch.zeros(1, device=dev)  # the runtime's threads exist before they are pinned
+    affinity0 = sorted(os.sched_getaffinity(0))
+    pinned = []
+    if args.pin_cpus > 0:
+        import splat_affinity
+        pinned = splat_affinity.pin_host_threads(local, local, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
+                                                 args.pin_cpus)
 
     if c5_cfg:
         cfg = S.SceneConfig("C5", 2_000_000, 1920, 1080, 1600.0, 0.005, views=S.RIG27)
@@ -1083,7 +1095,11 @@ def main():
             cam_cpu = S.render_settings(cfg.width, cfg.height, S.intrinsics(cfg.focal, cfg.width, cfg.height),
                                         S.look_at(yaw, hgt, cfg.distance), device="cpu",
                                         sh_degree=max(cfg.sh_degree, 0))
+            if pinned:  # the CPU baseline gets the process's whole CPU share back
+                splat_affinity.unpin_host_threads(affinity0)
             cpu = cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl.cpu(), args.cpu_threads)
+            if pinned:
+                splat_affinity.unpin_host_threads(pinned)
         workload = {
             "C2": f"C2: {cfg.P} Gaussians, RGB, {cfg.width}x{cfg.height}, the 4 cameras (yaw 0/90/180/270) "
                   f"per GPU per step, fwd+bwd" + (", RCCL SUM all-reduce of the gradients" if world > 1 else ""),
@@ -1123,7 +1139,8 @@ def main():
                        "submission": "one host thread per stream" if rstep.pool is not None else "one host thread",
                        "means2D": None if c5_cfg else ("one fresh zero leaf per render (shared.py:38-41)"
                                                        if args.means2d == "per-view" else "one leaf shared by the step's views"),
-                       "backend": args.backend if dist is not None else None},
+                       "backend": args.backend if dist is not None else None,
+                       "host_cpus": pinned or "unpinned"},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
