@@ -200,13 +200,13 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
 constexpr int kColW = GSR_COLSCAN_W, kColG = 32, kColR = 16;
 static_assert(kColG * kColR >= 512, "BinGrid makes at most 512 chunks");
 static_assert(kColW <= 64 && kMaxLdsTiles <= kColW * kScanBlocksMax, "look-back: one wave per block, <= kScanBlocksMax blocks");
-// Slab order inside a tile's range: the chunks that k_bin_emit runs on one XCD (blocks go round-robin
-// over the 8 XCDs: chunk b on XCD b % 8) are adjacent, so each XCD's scattered 16-byte pair stores
-// into a tile fill one contiguous run and the partial cache lines merge in that XCD's L2 instead of
-// being written back from up to 8 of them (pair writes were billed 2x their bytes).  The order inside
-// a tile is made canonical by the tile sort, so only placement changes.
+// Slab order inside a tile's range (GSR_XCD_SLABS=1, not the default): the chunks k_bin_emit would run
+// on one XCD under round-robin dispatch (chunk b on XCD b % 8) adjacent, so that XCD's scattered pair
+// stores into a tile form one run.  Measured against chunk order: k_bin_emit alone 47 vs 54 us, but its
+// written bytes 130 vs 102 MB per launch and, inside the 3-stream step, bin_emit 214-218 -> 327-341 us
+// and tile_sort 41 -> 99-148 us; the step 1354-1366 vs 1357-1381 Msplats/s (tools/r04_xcd_ab.sh).
 #ifndef GSR_XCD_SLABS
-#define GSR_XCD_SLABS 1
+#define GSR_XCD_SLABS 0
 #endif
 __device__ inline int slab_chunk(int k, int NB) {  // the chunk at slab position k of a tile's range
     if (!GSR_XCD_SLABS) return k;
