@@ -406,7 +406,7 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
 # kernels are VALU-bound and slow each other down when they share the chip, and the hand-off adds host
 # time -- 1014-1031 Msplats/s without, 955-970 with.
 _VIEW_STREAMS = {"on": os.environ.get("GSR_VIEW_STREAMS", "0") == "1", "n": int(os.environ.get("GSR_VIEW_STREAMS_N", "3")),
-                 "pool": {}, "next": {}}
+                 "pool": {}, "next": {}, "helper": os.environ.get("GSR_VIEW_HELPER", "1") != "0"}
 
 
 def set_view_streams(on: bool) -> bool:
@@ -495,7 +495,7 @@ def _on_view_stream(args, rs):
     for t in args:
         if t.numel() and t.is_cuda:
             t.record_stream(L)  # read on L (forward and backward): no early reuse on C
-    if _helper is None:
+    if _helper is None and _VIEW_STREAMS["helper"]:
         with _helper_lock:
             if _helper is None:
                 _helper = _HelperThread()
@@ -507,7 +507,10 @@ def _on_view_stream(args, rs):
                 return _RasterizeGaussians.apply(*args, rs, True)
             finally:
                 _view_tls.cur = None
-    color, radii, depth = _helper.call(job)
+    # without the helper the node gets the caller's sequence numbers: with ONE view stream the engine
+    # then runs view k's consumers (on C) before view k-1's rasterizer backward (on L), which still
+    # overlaps them
+    color, radii, depth = _helper.call(job) if _VIEW_STREAMS["helper"] else job()
     for t in (color, radii, depth):
         t.record_stream(C)
     evs[1].record(L)
