@@ -547,9 +547,15 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
                 if ((lane & 15) < kRedLanes) {  // the first kRedLanes lanes of each row hold its partial
                     // sums, added into the zeroed slot (2 lanes: 0 + h0 + h1 == h0 + h1 in either order)
                     float *o = s_out + j * kPartial;
+#if GSR_BWD_RED_STAGES >= 4
+                    o[xslot] = sm.X;  // one lane per row: every slot is written once per pair
+                    o[yslot] = sm.Y;
+                    if (lane == 0) o[5] = sm.Z;
+#else
                     lds_add(o + xslot, sm.X);
                     lds_add(o + yslot, sm.Y);
                     if (lane < kRedLanes) lds_add(o + 5, sm.Z);
+#endif
                 }
             }
 #endif

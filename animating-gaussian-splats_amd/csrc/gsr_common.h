@@ -809,7 +809,8 @@ __device__ inline float row_sum16_pairs(float v) {
 // a row hold them).  Row totals:
 //   X rows: [sum dx S0, sum S4, sum S1, sum cs0]    Y rows: [sum dx^2 S0, sum cs1, sum dx S1, sum cs2]
 //   Z row 0: sum S0
-// GSR_BWD_RED_STAGES: DPP stages of the row sums (3: lanes 0-1 of a row hold its halves; 2: lanes
+// GSR_BWD_RED_STAGES: DPP stages of the row sums (4: lane 0 of a row holds its total, stored plainly;
+// 3: lanes 0-1 of a row hold its halves; 2: lanes
 // 0-3 its quarters; 1: lanes 0-7 its eighths) -- the rest is added by LDS atomics into the slot
 #ifndef GSR_BWD_RED_STAGES
 #define GSR_BWD_RED_STAGES 3
@@ -821,6 +822,8 @@ __device__ inline float row_sum16_part(float v) {
         v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
     if (GSR_BWD_RED_STAGES >= 3)
         v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+    if (GSR_BWD_RED_STAGES >= 4)  // lane 0 of the row holds the whole row sum: a plain LDS store, no atomics
+        v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
     return v;
 }
 struct PairSums { float X, Y, Z; };

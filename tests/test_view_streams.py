@@ -93,8 +93,8 @@ def _densify_step(rs, params, dl):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("async_fwd", [True, False])
-def test_train_and_densify_shapes_bitwise(cuda, async_fwd):
+@pytest.mark.parametrize("async_fwd,n_streams,helper", [(True, 3, True), (False, 3, True), (False, 1, False)])
+def test_train_and_densify_shapes_bitwise(cuda, async_fwd, n_streams, helper):
     import splat_scenes as S
     P, W, H = 120_000, 640, 400
     base = S.synthetic_cloud(P, 0.008, seed=3, device=cuda)  # frozen (requires_grad False)
@@ -109,6 +109,9 @@ def test_train_and_densify_shapes_bitwise(cuda, async_fwd):
     params["segmentation_masks"] = torch.nn.Parameter((torch.rand(P, 1, generator=g) > 0.5).float().repeat(1, 3).to(cuda))
     prev_async = dgr.set_async_forward(async_fwd)
     prev = dgr.set_view_streams(False)
+    vs = dgr._VIEW_STREAMS
+    prev_cfg = vs["n"], vs["helper"], vs["pool"], vs["next"]
+    vs["n"], vs["helper"], vs["pool"], vs["next"] = n_streams, helper, {}, {}
     try:
         _train_step(cams, base, dl, delta)  # pair-count history for the asynchronous forwards
         _densify_step(cams[0], params, dl)
@@ -127,3 +130,4 @@ def test_train_and_densify_shapes_bitwise(cuda, async_fwd):
     finally:
         dgr.set_view_streams(prev)
         dgr.set_async_forward(prev_async)
+        vs["n"], vs["helper"], vs["pool"], vs["next"] = prev_cfg
