@@ -499,9 +499,22 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
                 // branch-free: a non-contributing pixel gets alpha = 0, which makes every update an
                 // identity (r = 1, AR unchanged, zero sums)
                 const float dy = a.y - pfy[k];  // same operation as the forward's (bitwise-equal decisions)
+#if GSR_EXACT_NEAR
+                float p2 = pair_power(x, b.x, dy);
+                float G = __builtin_amdgcn_exp2f(p2);
+                float alpha = fminf(0.99f, b.y * G);
+                {   // the forward's near-threshold re-evaluation, so both take the same decisions
+                    const bool nr = p < lastc[k] && near_threshold(alpha);
+                    if (__ballot(nr) && nr) {
+                        const uint32_t g = point_list[rg.x + p];
+                        exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy[k], p2, G, alpha);
+                    }
+                }
+#else
                 const float p2 = pair_power(x, b.x, dy);
                 const float G = __builtin_amdgcn_exp2f(p2);
                 const float alpha = fminf(0.99f, b.y * G);
+#endif
                 const bool ok = p < lastc[k] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
                 any = any || ok;
                 const float al = ok ? alpha : 0.f;

@@ -603,6 +603,28 @@ __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
 }
 __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }
 
+// Near-threshold exact blend weight (GSR_EXACT_NEAR=1): the fast weight
+// 2^(p2) (FMAs on log2(e)-scaled conic terms + v_exp_f32) differs from the reference's
+// expf(-0.5 (a dx^2 + c dy^2) - b dx dy) by a few ulp, so a pair whose weight lies within kNearRel of
+// 1/255 can take the other branch.  Such pairs (rare: the wave branches only when a lane has one) are
+// re-evaluated with the reference's expression order in fp32 (the library builds with
+// -ffp-contract=off, like the oracle) and a double-precision exp rounded to float, from the exact
+// conic kept in the render record's 4th float4.
+#ifndef GSR_EXACT_NEAR
+#define GSR_EXACT_NEAR 0
+#endif
+constexpr float kNearRel = 1e-5f;
+constexpr float kNearLo = (1.0f / 255.0f) * (1.0f - kNearRel), kNearHi = (1.0f / 255.0f) * (1.0f + kNearRel);
+__device__ inline bool near_threshold(float alpha) { return alpha >= kNearLo && alpha < kNearHi; }
+// exact (power, G, alpha) of the Gaussian at (gx, gy) with exact conic (ca, cb, cc) and opacity o
+__device__ __attribute__((noinline)) void exact_blend(float gx, float gy, float4 conic, float o, float pfx, float pfy, float &power,
+                                   float &G, float &alpha) {
+    const float dx = gx - pfx, dy = gy - pfy;
+    power = -0.5f * (conic.x * dx * dx + conic.z * dy * dy) - conic.y * dx * dy;
+    G = (float)exp((double)power);
+    alpha = fminf(0.99f, o * G);
+}
+
 // A workgroup barrier after this wave's LDS stores / no-return LDS atomics, with an explicit
 // s_waitcnt lgkmcnt(0) in front.  __syncthreads()'s release fence normally brings that wait, but the
 // compiler dropped it in one build at k_render_fwd's blend-loop head (its loop-carried s_live mask,

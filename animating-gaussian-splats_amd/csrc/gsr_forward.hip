@@ -1029,7 +1029,18 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const int j = __builtin_ctzll(m);
             m &= m - 1;
             const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
+#if GSR_EXACT_NEAR
+            Blend e = blend_eval(a, b, pfx, pfy);
+            const bool nr = thr < kThrDone && near_threshold(e.alpha);
+            if (__ballot(nr) && nr) {
+                const int idx = base + j;
+                const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
+                exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy, e.p2, e.G, e.alpha);
+            }
+            take(e, b, c, j);
+#else
             take(blend_eval(a, b, pfx, pfy), b, c, j);
+#endif
         }
         if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
