@@ -10,13 +10,18 @@ for v in def exact; do
 done
 python3 - <<'PY'
 import json
+from collections import defaultdict
+PIX = {"n_contrib", "final_T", "color", "depth"}
 for v in ("def", "exact"):
     try:
         d = json.load(open(f"gpurun_out/r04/parity_stats_{v}.json"))
     except OSError:
         print(v, "no stats"); continue
-    for t, r in sorted(d.items()):
-        if isinstance(r, dict) and "max_grad_frac" in r:
-            print(v, t, "pix", r.get("max_pixel_frac"), "grad", r.get("max_grad_frac"))
+    pix, grad = defaultdict(float), defaultdict(float)
+    for row in d:
+        t, f, frac = row[0], row[1], row[2]
+        (pix if f in PIX else grad)[t] = max((pix if f in PIX else grad)[t], frac)
+    for t in sorted(set(pix) | set(grad)):
+        print(v, t.split("::")[-1], "pix %.2e grad %.2e" % (pix[t], grad[t]))
 PY
 bash tools/r04_lib_ab.sh exact 2
