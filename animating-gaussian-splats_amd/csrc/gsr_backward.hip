@@ -507,7 +507,8 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
                     const bool nr = p < lastc[k] && near_threshold(alpha);
                     if (__ballot(nr) && nr) {
                         const uint32_t g = point_list[rg.x + p];
-                        exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy[k], p2, G, alpha);
+                        const ExactBlend e = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy[k]);
+                        p2 = e.power; G = e.G; alpha = e.alpha;
                     }
                 }
 #else

@@ -616,13 +616,18 @@ __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha
 constexpr float kNearRel = 1e-5f;
 constexpr float kNearLo = (1.0f / 255.0f) * (1.0f - kNearRel), kNearHi = (1.0f / 255.0f) * (1.0f + kNearRel);
 __device__ inline bool near_threshold(float alpha) { return alpha >= kNearLo && alpha < kNearHi; }
-// exact (power, G, alpha) of the Gaussian at (gx, gy) with exact conic (ca, cb, cc) and opacity o
-__device__ __attribute__((noinline)) void exact_blend(float gx, float gy, float4 conic, float o, float pfx, float pfy, float &power,
-                                   float &G, float &alpha) {
+// exact (power, G, alpha) of the Gaussian at (gx, gy) with exact conic (ca, cb, cc) and opacity o.  Not
+// inlined (the double-precision exp would hold registers in the hot loops) and returned by value (a
+// by-reference output would put the caller's blend variables in scratch memory).
+struct ExactBlend { float power, G, alpha; };
+__device__ __attribute__((noinline)) ExactBlend exact_blend(float gx, float gy, float4 conic, float o, float pfx,
+                                                            float pfy) {
     const float dx = gx - pfx, dy = gy - pfy;
-    power = -0.5f * (conic.x * dx * dx + conic.z * dy * dy) - conic.y * dx * dy;
-    G = (float)exp((double)power);
-    alpha = fminf(0.99f, o * G);
+    ExactBlend r;
+    r.power = -0.5f * (conic.x * dx * dx + conic.z * dy * dy) - conic.y * dx * dy;
+    r.G = (float)exp((double)r.power);
+    r.alpha = fminf(0.99f, o * r.G);
+    return r;
 }
 
 // A workgroup barrier after this wave's LDS stores / no-return LDS atomics, with an explicit

@@ -1035,7 +1035,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             if (__ballot(nr) && nr) {
                 const int idx = base + j;
                 const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
-                exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy, e.p2, e.G, e.alpha);
+                const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
+                e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
             }
             take(e, b, c, j);
 #else
