@@ -17,6 +17,7 @@
 #include <map>
 #include <memory>
 #include <unordered_map>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -199,8 +200,15 @@ int check_common(const gsr_camera *cam, const gsr_gaussians *g, bool need_opacit
     return GSR_OK;
 }
 
+// exact-threshold mode (gsr_set_exact_thresholds; GSR_EXACT_THRESHOLDS=1 at load)
+std::atomic<int> g_exact{[] {
+    const char *e = getenv("GSR_EXACT_THRESHOLDS");
+    return (e && e[0] == '1') ? 1 : 0;
+}()};
+
 void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
     memset(&a, 0, sizeof(a));
+    a.exact = g_exact.load(std::memory_order_relaxed);
     a.P = g->P; a.D = g->sh_degree; a.M = g->shs ? g->sh_coeffs : 0;
     a.W = cam->image_width; a.H = cam->image_height;
     a.gx = div_up(a.W, kTileW); a.gy = div_up(a.H, kTileH);
@@ -251,6 +259,8 @@ void carve_binning(FwdArgs &a, char *base, int K) {
 extern "C" {
 
 const char *gsr_last_error(void) { return g_err.c_str(); }
+
+int gsr_set_exact_thresholds(int on) { return g_exact.exchange(on ? 1 : 0); }
 int gsr_abi_version(void) { return GSR_ABI_VERSION; }
 
 size_t gsr_geom_bytes(int P) { return GeomLayout(P < 0 ? 0 : P).total; }
@@ -1022,7 +1032,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.radii = radii;
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff; a.clampm = f.clampm;
     a.ranges = f.ranges; a.pix_end = f.pix_end; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
-    a.seg_off = f.seg_off; a.meta = f.meta; a.items_ws = f.items_ws;
+    a.seg_off = f.seg_off; a.meta = f.meta; a.items_ws = f.items_ws; a.exact = f.exact;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
     a.dL_dcolor = dL_dcolor;
     const ScratchLayout SL(num_rendered, a.gx * a.gy);

@@ -243,6 +243,7 @@ constexpr int kBwdWaves = GSR_BWD_WAVES;
 constexpr int kTred = GSR_BWD_TRED;
 constexpr int kTredF = 96;  // floats per parked pair: 4 column-sum rows (64) + cs1 / cs2 columns (32)
 #endif
+template <bool EXACT>
 __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
@@ -499,11 +500,10 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
                 // branch-free: a non-contributing pixel gets alpha = 0, which makes every update an
                 // identity (r = 1, AR unchanged, zero sums)
                 const float dy = a.y - pfy[k];  // same operation as the forward's (bitwise-equal decisions)
-#if GSR_EXACT_NEAR
                 float p2 = pair_power(x, b.x, dy);
                 float G = __builtin_amdgcn_exp2f(p2);
                 float alpha = fminf(0.99f, b.y * G);
-                {   // the forward's near-threshold re-evaluation, so both take the same decisions
+                if constexpr (EXACT) {  // the forward's near-threshold re-evaluation: the same decisions
                     const bool nr = p < lastc[k] && near_threshold(alpha);
                     if (__ballot(nr) && nr) {
                         const uint32_t g = point_list[rg.x + p];
@@ -511,11 +511,6 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
                         p2 = e.power; G = e.G; alpha = e.alpha;
                     }
                 }
-#else
-                const float p2 = pair_power(x, b.x, dy);
-                const float G = __builtin_amdgcn_exp2f(p2);
-                const float alpha = fminf(0.99f, b.y * G);
-#endif
                 const bool ok = p < lastc[k] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
                 any = any || ok;
                 const float al = ok ? alpha : 0.f;
@@ -1356,9 +1351,10 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     if (a.K == 0) return hipSuccess;
     // one wave per item, kBwdWaves per workgroup; the launch covers the item bound, waves without an
     // item exit at once
-    k_render_bwd<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
-                                             a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
-                                             a.slot_emit, a.dL_dcolor, a.part, seg_log2(a.P));
+    auto k = a.exact ? k_render_bwd<true> : k_render_bwd<false>;
+    k<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
+                                                                     a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
+                                                                     a.slot_emit, a.dL_dcolor, a.part, seg_log2(a.P));
     return hipGetLastError();
 }
 

@@ -603,16 +603,14 @@ __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
 }
 __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }
 
-// Near-threshold exact blend weight (GSR_EXACT_NEAR=1): the fast weight
+// Near-threshold exact blend weight (exact-threshold mode, gsr_set_exact_thresholds, VERDICT r03
+// item 9): the fast weight
 // 2^(p2) (FMAs on log2(e)-scaled conic terms + v_exp_f32) differs from the reference's
 // expf(-0.5 (a dx^2 + c dy^2) - b dx dy) by a few ulp, so a pair whose weight lies within kNearRel of
 // 1/255 can take the other branch.  Such pairs (rare: the wave branches only when a lane has one) are
 // re-evaluated with the reference's expression order in fp32 (the library builds with
 // -ffp-contract=off, like the oracle) and a double-precision exp rounded to float, from the exact
 // conic kept in the render record's 4th float4.
-#ifndef GSR_EXACT_NEAR
-#define GSR_EXACT_NEAR 0
-#endif
 constexpr float kNearRel = 1e-5f;
 constexpr float kNearLo = (1.0f / 255.0f) * (1.0f - kNearRel), kNearHi = (1.0f / 255.0f) * (1.0f + kNearRel);
 __device__ inline bool near_threshold(float alpha) { return alpha >= kNearLo && alpha < kNearHi; }

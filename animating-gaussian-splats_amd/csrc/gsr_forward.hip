@@ -868,6 +868,7 @@ __device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *e
     }
 }
 
+template <bool EXACT>
 __global__ __launch_bounds__(256) void k_render_fwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
     const uint4 *__restrict__ pairs,
@@ -1029,19 +1030,19 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const int j = __builtin_ctzll(m);
             m &= m - 1;
             const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
-#if GSR_EXACT_NEAR
-            Blend e = blend_eval(a, b, pfx, pfy);
-            const bool nr = thr < kThrDone && near_threshold(e.alpha);
-            if (__ballot(nr) && nr) {
-                const int idx = base + j;
-                const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
-                const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
-                e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
+            if constexpr (EXACT) {
+                Blend e = blend_eval(a, b, pfx, pfy);
+                const bool nr = thr < kThrDone && near_threshold(e.alpha);
+                if (__ballot(nr) && nr) {
+                    const int idx = base + j;
+                    const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
+                    const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
+                    e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
+                }
+                take(e, b, c, j);
+            } else {
+                take(blend_eval(a, b, pfx, pfy), b, c, j);
             }
-            take(e, b, c, j);
-#else
-            take(blend_eval(a, b, pfx, pfy), b, c, j);
-#endif
         }
         if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
@@ -1190,10 +1191,11 @@ hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, 
 
 hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     const int T = a.gx * a.gy;
-    k_render_fwd<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
-                                   a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
-                                   a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
-                                   a.gate_err);
+    auto k = a.exact ? k_render_fwd<true> : k_render_fwd<false>;
+    k<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
+                        a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
+                        a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
+                        a.gate_err);
     return hipGetLastError();
 }
 

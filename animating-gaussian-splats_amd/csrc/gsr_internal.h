@@ -30,6 +30,8 @@ struct FwdArgs {
     // asynchronous forward (gsr_forward_async): the gate word the speculative render's first wave waits
     // on when the speculation failed, the value that opens it, and the timeout error word
     const uint32_t *gate; uint32_t gate_seq; uint32_t *gate_err;
+    // exact-threshold mode (gsr_set_exact_thresholds): near-threshold blend weights re-evaluated
+    int exact;
 };
 // blocks of the speculative k_tile_sort launch (they loop over the device-side list count)
 constexpr int kSpecSortBlocks = 512;
@@ -55,6 +57,7 @@ struct BwdArgs {
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
         *dL_drot;
     int accm;  // gsr_grad_bits: outputs accumulated into instead of overwritten
+    int exact;  // exact-threshold mode (the forward's)
 };
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);

@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
     "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes", "gsr_prealloc_alloc", "gsr_spec_binning_bytes",
     "gsr_forward_async", "gsr_forward_resolve", "gsr_forward_release", "gsr_forward_query", "gsr_async_stats",
-    "gsr_spec_keys", "gsr_async_shutdown",
+    "gsr_spec_keys", "gsr_async_shutdown", "gsr_set_exact_thresholds",
 )
 
 
@@ -176,6 +176,8 @@ def load_library():
     L.gsr_l1_ssim_backward.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, vp]
     L.gsr_spec_binning_bytes.restype = ctypes.c_size_t
     L.gsr_spec_binning_bytes.argtypes = [i, i, i, i]
+    L.gsr_set_exact_thresholds.restype = i
+    L.gsr_set_exact_thresholds.argtypes = [i]
     if L.gsr_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libgsr.so ABI {L.gsr_abi_version()} != binding ABI {ABI_VERSION}: rebuild it")
     global _PREALLOC_FN
@@ -184,9 +186,16 @@ def load_library():
     return L
 
 
-ABI_VERSION = 17  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 18  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
+
+
+def set_exact_thresholds(on: bool) -> bool:
+    """Exact-threshold mode (gsr_set_exact_thresholds, ABI 18): blend weights within 1e-5 of the 1/255
+    threshold re-evaluated in the reference's expression order, so the forward and backward take the
+    reference's decisions there.  Process-wide; returns the previous setting."""
+    return bool(load_library().gsr_set_exact_thresholds(int(bool(on))))
 
 
 def _check(rc):

@@ -24,7 +24,7 @@ from torch.autograd.graph import get_gradient_edge
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "set_async_forward", "async_forward",
+           "rasterize_parameters", "set_deferred_backward", "set_speculative_forward", "set_async_forward", "async_forward", "set_exact_thresholds",
            "pending_views", "clear_pending"]
 
 
@@ -179,6 +179,13 @@ def set_speculative_forward(on: bool) -> bool:
     prev = _defer["speculate"]
     _defer["speculate"] = bool(on)
     return prev
+
+
+def set_exact_thresholds(on: bool) -> bool:
+    """Exact-threshold mode (include/gsr.h gsr_set_exact_thresholds): near-threshold blend weights
+    re-evaluated as the reference computes them (~15 % render-kernel time); returns the previous
+    setting.  Set it before a forward and keep it until that forward's backward has run."""
+    return _C.set_exact_thresholds(on)
 
 
 def set_async_forward(on: bool) -> bool:

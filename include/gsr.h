@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 17
+#define GSR_ABI_VERSION 18
 
 enum gsr_status {
     GSR_OK = 0,
@@ -313,6 +313,17 @@ int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *o
 
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
+
+/* Exact-threshold mode (ABI >= 18; process-wide, off by default, GSR_EXACT_THRESHOLDS=1 at load turns
+ * it on).  The render kernels evaluate the blend weight as 2^(power log2 e) with FMAs and the hardware
+ * exp, which differs from the reference's expf(power) (renderCUDA, forward.cu / backward.cu) by a few
+ * ulp; a (pixel, Gaussian) weight that close to 1/255 can take the other side of the threshold.  With
+ * the mode on, such weights (within 1e-5 relative of 1/255) are re-evaluated with the reference's
+ * expression order and a double-precision exp, in the forward and the backward alike, so decisions
+ * match the reference's (measured: blend-decision flips 1.5e-5 -> 0 of the pixels on the densest test
+ * case) at ~15 % render-kernel time.  Set it before a forward and keep it until that
+ * forward's backward has been queued.  Returns the previous setting. */
+int gsr_set_exact_thresholds(int on);
 
 /* ---- Fused L1 + SSIM image loss (ABI >= 3) ------------------------------
  * Replaces the loss of every render call site, train.py:362-363 / densify.py:127-129,149-151:
