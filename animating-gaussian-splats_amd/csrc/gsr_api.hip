@@ -320,6 +320,7 @@ constexpr int kSpecWindow = 16;
 constexpr size_t kSpecKeys = 64;
 struct SpecStat {
     uint32_t recent[kSpecWindow] = {};
+    uint32_t recent_mid[kSpecWindow] = {};  // lists sorted by k_tile_sort (1024 < n <= 4096)
     int n = 0;
     bool long_lists = false;
     uint64_t used = 0;
@@ -334,16 +335,24 @@ std::unordered_map<SpecKey, SpecStat, SpecKeyHash> g_spec;
 uint64_t g_spec_clock = 0;
 int g_spec_hits = 0, g_spec_misses = 0, g_async_calls = 0;
 
-uint32_t spec_capacity(const SpecKey &key) {
+// The speculative capacity of a key (0: no history / long lists) and, in *sort_blocks, the grid of the
+// speculative k_tile_sort (its blocks loop over the device-side list count; a grid near the recent
+// counts instead of kSpecSortBlocks keeps hundreds of idle 48 KB-LDS blocks out of a busy chip).
+uint32_t spec_capacity(const SpecKey &key, uint32_t *sort_blocks = nullptr) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     auto it = g_spec.find(key);
     if (it == g_spec.end() || it->second.long_lists) return 0;
     it->second.used = ++g_spec_clock;
     const uint32_t mk = it->second.window_max();
+    if (sort_blocks) {
+        uint32_t mm = 0;
+        for (int k = 0; k < std::min(it->second.n, kSpecWindow); ++k) mm = std::max(mm, it->second.recent_mid[k]);
+        *sort_blocks = std::min<uint32_t>((uint32_t)kSpecSortBlocks, mm + mm / 4 + 16);
+    }
     const uint64_t c = (uint64_t)mk + mk / 4 + 65536;
     return (uint32_t)std::min<uint64_t>((c + 4095) & ~uint64_t(4095), 0x7FFFFFFFu);
 }
-void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
+void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome, uint32_t n_mid) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     if (!g_spec.count(key) && g_spec.size() >= kSpecKeys) {  // evict the least recently used key
         auto lru = g_spec.begin();
@@ -353,6 +362,7 @@ void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome) {
     }
     SpecStat &st = g_spec[key];
     st.recent[st.n % kSpecWindow] = K;
+    st.recent_mid[st.n % kSpecWindow] = n_mid;
     ++st.n;
     st.long_lists = long_lists;
     st.used = ++g_spec_clock;
@@ -547,15 +557,15 @@ int slot_acquire() {
 void async_classify(AsyncFwd &f) {
     const uint32_t *w = slot_h(f.slot);
     f.K = __atomic_load_n(w, __ATOMIC_ACQUIRE);
-    const uint32_t n_vlong = __atomic_load_n(w + 2, __ATOMIC_ACQUIRE);
+    const uint32_t n_vlong = __atomic_load_n(w + 2, __ATOMIC_ACQUIRE), n_mid = __atomic_load_n(w + 1, __ATOMIC_ACQUIRE);
     if (f.K <= f.cap && n_vlong == 0) {  // the device's verdict (k_bin_scan: K <= cap, no merge-sorted list)
         f.state = 1;
         f.layout = (int)f.cap;
         f.bin = f.spec_bin;
-        spec_record(f.key, f.K, false, +1);
+        spec_record(f.key, f.K, false, +1, n_mid);
     } else {
         f.state = 2;
-        spec_record(f.key, f.K, n_vlong > 0, -1);
+        spec_record(f.key, f.K, n_vlong > 0, -1, n_mid);
     }
 }
 
@@ -716,8 +726,10 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     int dev = 0;
     (void)hipGetDevice(&dev);
     const SpecKey key{dev, a.P, a.W, a.H};
-    const uint32_t cap = mode ? spec_capacity(key) : 0u;
+    uint32_t sort_blocks = kSpecSortBlocks;
+    const uint32_t cap = mode ? spec_capacity(key, &sort_blocks) : 0u;
     a.spec_cap = cap;
+    a.spec_sort_blocks = sort_blocks;
     const int T = a.gx * a.gy;
     // where k_bin_scan publishes K: an asynchronous forward's ring slot, else this thread's word
     std::shared_ptr<AsyncFwd> af;
@@ -837,7 +849,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     if (cap && K <= cap && n_vlong == 0) {  // the device took the same verdict: the queued work stands
         info->binning_layout = (int)cap;
         info->speculated = 1;
-        spec_record(key, K, false, +1);
+        spec_record(key, K, false, +1, n_mid);
         return GSR_OK;
     }
     // exact path (also the redo of a failed speculation: its queued kernels returned at once)
@@ -862,7 +874,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         if (used) info->aux_stream = used;
     }
     info->binning_layout = (int)K;
-    spec_record(key, K, n_vlong > 0, cap ? -1 : 0);
+    spec_record(key, K, n_vlong > 0, cap ? -1 : 0, n_mid);
     return GSR_OK;
 }
 }  // namespace

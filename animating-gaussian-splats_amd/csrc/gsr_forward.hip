@@ -1166,7 +1166,8 @@ hipError_t launch_tile_sort(const FwdArgs &a, uint32_t n_mid, uint32_t n_vlong, 
     // per tile; longer ones by chunk sorts + merge passes
     const int T = a.gx * a.gy;
     if (a.spec_ok) {  // speculative: the count is on the device; blocks loop over it (none here: n_vlong == 0)
-        k_tile_sort<<<std::min(T, kSpecSortBlocks), 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs, a.point_list,
+        const int nb = a.spec_sort_blocks ? (int)a.spec_sort_blocks : kSpecSortBlocks;
+        k_tile_sort<<<std::min(T, nb), 512, 0, s>>>(a.gx, a.sort_lists, a.ranges, a.pairs, a.point_list,
                                                                  a.slot_emit, 0u, a.spec_ok);
         return hipGetLastError();
     }

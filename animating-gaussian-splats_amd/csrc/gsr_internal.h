@@ -27,6 +27,7 @@ struct FwdArgs {
     // were queued with before the host read K (0: exact path), and the device flag they check
     // (meta + 1, written by k_bin_scan; nullptr: exact path)
     uint32_t spec_cap; const uint32_t *spec_ok;
+    uint32_t spec_sort_blocks;  // grid of the speculative k_tile_sort (<= kSpecSortBlocks; 0: that bound)
     // asynchronous forward (gsr_forward_async): the gate word the speculative render's first wave waits
     // on when the speculation failed, the value that opens it, and the timeout error word
     const uint32_t *gate; uint32_t gate_seq; uint32_t *gate_err;
