@@ -14,6 +14,9 @@ from diff_gaussian_rasterization import _C  # noqa: E402
 
 dev = torch.device("cuda", 0)
 _C.load_library()
+torch.zeros(1, device=dev)
+import splat_affinity  # noqa: E402
+print("pinned", splat_affinity.pin_host_threads(0, 0, 1, 8))
 r = bench.c2_leg(100, 10, dev)
 print({k: r[k] for k in ("Msplats_per_s", "median_ms_per_step", "host_ms_per_step_median")})
 pr = cProfile.Profile()
@@ -22,5 +25,5 @@ r = bench.c2_leg(200, 10, dev)
 pr.disable()
 print({k: r[k] for k in ("Msplats_per_s", "median_ms_per_step", "host_ms_per_step_median")})
 st = pstats.Stats(pr)
-st.sort_stats("tottime").print_stats(35)
+st.sort_stats("tottime").print_stats(45)
 st.sort_stats("cumulative").print_stats(45)
