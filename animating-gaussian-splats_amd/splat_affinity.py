@@ -25,14 +25,49 @@ def _cpulist(text):
     return out
 
 
+def _numa_of_bdf(bdf):
+    try:
+        return int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+    except (OSError, ValueError):
+        return -1
+
+
+def _gpu_numa_node_sysfs(dev_index):
+    """NUMA node of visible GPU ``dev_index`` without initialising the GPU runtime: HIP_VISIBLE_DEVICES
+    / ROCR_VISIBLE_DEVICES map it to a ROCr index, the KFD topology's GPU nodes (in ROCr order) give
+    its PCI location.  -1 when unknown."""
+    try:
+        idx = dev_index
+        for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES"):
+            v = os.environ.get(var)
+            if v:
+                idx = int(v.split(",")[idx])
+        base = "/sys/class/kfd/kfd/topology/nodes"
+        gpus = []
+        for n in sorted(os.listdir(base), key=int):
+            props = {}
+            for line in open(os.path.join(base, n, "properties")):
+                k, _, val = line.partition(" ")
+                props[k] = val.strip()
+            if int(props.get("simd_count", "0")) > 0:
+                gpus.append(props)
+        loc, dom = int(gpus[idx]["location_id"]), int(gpus[idx].get("domain", "0"))
+        return _numa_of_bdf(f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 31:02x}.{loc & 7}")
+    except (OSError, ValueError, IndexError, KeyError):
+        return -1
+
+
 def _gpu_numa_node(dev_index):
-    """NUMA node of the visible GPU ``dev_index`` (-1 when unknown), from its PCI address."""
+    """NUMA node of the visible GPU ``dev_index`` (-1 when unknown), from its PCI address: from sysfs
+    first (no GPU runtime needed), else from the runtime's device properties."""
+    node = _gpu_numa_node_sysfs(dev_index)
+    if node >= 0:
+        return node
     try:
         import torch
         pr = torch.cuda.get_device_properties(dev_index)
-        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
-        return int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
-    except (AttributeError, OSError, ValueError, RuntimeError):
+        return _numa_of_bdf(f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0")
+    except (AttributeError, RuntimeError):
         return -1
 
 
@@ -87,7 +122,8 @@ def choose_cpus(dev_index=0, local_rank=0, local_world=1, n=8):
 
 def pin_host_threads(dev_index=0, local_rank=0, local_world=1, n=8):
     """Pin every thread of this process to ``choose_cpus(...)``; returns the CPUs (or [] when unpinned).
-    Call it once the GPU is initialised (so the runtime's threads exist and get pinned too)."""
+    Best called before the GPU runtime starts (its threads and its host allocations then start on those
+    CPUs and their NUMA node); threads that already exist are pinned too."""
     cpus = choose_cpus(dev_index, local_rank, local_world, n)
     if not cpus:
         return []

@@ -714,7 +714,7 @@ def main():
                     help="CPU rehearsal of the launcher / sharding / collective (gloo, no GPU work)")
     ap.add_argument("--pin-cpus", type=int, default=int(os.environ.get("GSR_PIN_CPUS", "8")),
                     help="pin the process's threads to this many of the least busy CPUs of the GPU's NUMA "
-                         "node (this rank's share of it) once the GPU is up -- a launcher's numactl; the "
+                         "node (this rank's share of it) before the GPU runtime starts -- a launcher's numactl; the "
                          "submitting threads otherwise wander over the shared host's 256 CPUs (0 = off; "
                          "splat_affinity.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -775,6 +775,14 @@ def main():
 
     dist = None
     local = local % max(torch.cuda.device_count(), 1)  # rehearsal: several gloo ranks on one GPU
+    # host-thread placement before the GPU runtime starts, so its threads and host allocations start on
+    # the chosen CPUs' node (pinning after it started: C2 399-473 vs 509-520 Msplats/s, tools/c2_pin.py)
+    affinity0 = sorted(os.sched_getaffinity(0))
+    pinned = []
+    if args.pin_cpus > 0:
+        import splat_affinity
+        pinned = splat_affinity.pin_host_threads(local, local, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
+                                                 args.pin_cpus)
     # under a launcher (torch.distributed.run sets WORLD_SIZE) the process group is formed even for one
     # rank, so `torchrun --nproc-per-node 1 bench.py --backend nccl` runs the RCCL path on one GPU
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
@@ -789,13 +797,6 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     _C.load_library()
-    torch.zeros(1, device=dev)  # the runtime's threads exist before they are pinned
-    affinity0 = sorted(os.sched_getaffinity(0))
-    pinned = []
-    if args.pin_cpus > 0:
-        import splat_affinity
-        pinned = splat_affinity.pin_host_threads(local, local, int(os.environ.get("LOCAL_WORLD_SIZE", "1")),
-                                                 args.pin_cpus)
 
     if c5_cfg:
         cfg = S.SceneConfig("C5", 2_000_000, 1920, 1080, 1600.0, 0.005, views=S.RIG27)

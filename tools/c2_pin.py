@@ -33,6 +33,9 @@ elif mode == "gpu":
     os.sched_setaffinity(0, node_cpus(max(gnode, 0)))
 elif mode.startswith("first"):
     os.sched_setaffinity(0, node_cpus(max(gnode, 0))[:int(mode[5:])])
+if mode == "early":  # bench.py's placement, before the GPU runtime starts
+    import splat_affinity
+    print("early", splat_affinity.pin_host_threads(0, 0, 1, 8), flush=True)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -40,6 +43,10 @@ from diff_gaussian_rasterization import _C  # noqa: E402
 
 dev = torch.device("cuda", 0)
 _C.load_library()
+if mode == "late":  # pinned after the runtime started
+    torch.zeros(1, device=dev)
+    import splat_affinity
+    print("late", splat_affinity.pin_host_threads(0, 0, 1, 8), flush=True)
 if mode == "none":
     pr = torch.cuda.get_device_properties(0)
     print({k: getattr(pr, k) for k in dir(pr) if "pci" in k.lower() or "uuid" in k.lower()}, flush=True)

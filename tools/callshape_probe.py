@@ -11,6 +11,8 @@ import time
 
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path[:0] = [os.path.join(REPO, "animating-gaussian-splats_amd"), REPO]
+import splat_affinity  # noqa: E402
+splat_affinity.pin_host_threads(0, 0, 1, int(os.environ.get("GSR_PIN_CPUS", "8")))  # as bench.py does
 import torch  # noqa: E402
 
 import bench  # noqa: E402
@@ -31,9 +33,6 @@ dgr.set_async_forward(not args.no_async)
 dgr.set_view_streams(not args.no_view_streams)
 dev = torch.device("cuda", 0)
 _C.load_library()
-torch.zeros(1, device=dev)
-import splat_affinity  # noqa: E402
-splat_affinity.pin_host_threads(0, 0, 1, int(os.environ.get("GSR_PIN_CPUS", "8")))  # as bench.py does
 base = S.CONFIGS["C3"]
 cfg = S.SceneConfig("C3", base.P, base.width, base.height, base.focal, base.s0, sh_degree=base.sh_degree,
                     views=S.RIG27)
