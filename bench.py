@@ -522,7 +522,9 @@ def unchanged_call_site(steps, warmup, cfg, cams, views, dl, dev):
     stacked, summed and backpropagated once (train.py:402-418, 767).  The loss of a view is
     ``(image * dL/dimage).sum()`` with the headline's fixed upstream gradient (the L1 + SSIM and the
     rigidity loss are out of the metric's scope).  Rasterizer inputs are not leaves, so every view
-    takes the immediate per-view backward; forwards return without a host wait (gsr_forward_async)."""
+    takes the immediate per-view backward.  Library defaults throughout: each forward reads its pair
+    count back as the reference's does (the asynchronous forward and the library view streams are off,
+    DESIGN.md 2.4d, as they measured slower on this shape)."""
     import splat_scenes as S
     from diff_gaussian_rasterization import GaussianRasterizer
     P = cfg.P
