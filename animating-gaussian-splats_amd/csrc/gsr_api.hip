@@ -1024,7 +1024,12 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
                     gsr_alloc_fn alloc, void *alloc_ctx, hipStream_t s, BwdArgs &a, bool sums = false) {
     if (!geom || !binning || !image || !dL_dcolor || !radii || !alloc)
         return fail(GSR_ERR_ARG, "gsr_backward: missing saved buffers / dL_dcolor / allocator");
-    if (num_rendered < 0) return fail(GSR_ERR_ARG, "num_rendered < 0");
+    // num_rendered < 0: a speculative render half (ABI 19) -- an asynchronous forward whose pair count is
+    // not known yet, queued against its capacity (binning_layout) and its own BINNING; its kernels
+    // return at once when the device's speculation verdict (the forward's meta[1]) failed, and the
+    // caller redoes the half once gsr_forward_resolve reports the forward redone
+    const bool spec = num_rendered < 0;
+    if (spec && g->binning_layout <= 0) return fail(GSR_ERR_ARG, "num_rendered < 0 without the forward's binning_layout");
     FwdArgs f;
     fill_common(f, cam, g);
     carve_geom(f, (char *)geom);
@@ -1032,6 +1037,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     // the BINNING layout the forward used: its capacity when it enqueued speculatively (gsr_forward_info)
     const int layout = g->binning_layout > 0 ? g->binning_layout : num_rendered;
     if (layout < num_rendered) return fail(GSR_ERR_ARG, "binning_layout %d < num_rendered %d", layout, num_rendered);
+    if (spec) num_rendered = layout;  // the bound every size below is taken from
     carve_binning(f, (char *)binning, layout);
     memset(&a, 0, sizeof(a));
     a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
@@ -1047,6 +1053,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.seg_off = f.seg_off; a.meta = f.meta; a.items_ws = f.items_ws; a.exact = f.exact;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
     a.dL_dcolor = dL_dcolor;
+    a.spec_ok = spec ? f.meta + 1 : nullptr;
     const ScratchLayout SL(num_rendered, a.gx * a.gy);
     char *scr = (char *)alloc(alloc_ctx, GSR_BUF_SCRATCH, SL.total);
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
@@ -1065,7 +1072,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
         float *out = (float *)alloc(alloc_ctx, GSR_BUF_SUMS, gsr_sums_bytes(a.P));
         if (!out) return fail(GSR_ERR_ALLOC, "allocation callback failed (sums)");
         Phase ph(s, "sum_records");
-        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s));
+        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s, a.spec_ok));
     }
     return GSR_OK;
 }
@@ -1084,6 +1091,7 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
     if (!out) return fail(GSR_ERR_ARG, "gsr_backward: null grads");
     if (g->P == 0) return GSR_OK;
     if (out->accumulate & ~0xFF) return fail(GSR_ERR_ARG, "gsr_backward: unknown accumulate bits 0x%x", out->accumulate);
+    if (num_rendered < 0) return fail(GSR_ERR_ARG, "gsr_backward: num_rendered < 0 (resolve the forward first)");
     hipStream_t s = (hipStream_t)stream;
     BwdArgs a;
     rc = backward_render(cam, g, radii, num_rendered, geom, binning, image, dL_dcolor, alloc, alloc_ctx, s, a);

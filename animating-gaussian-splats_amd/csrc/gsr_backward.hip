@@ -251,7 +251,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
-    float4 *__restrict__ part, int ks) {
+    float4 *__restrict__ part, int ks, const uint32_t *__restrict__ spec_ok) {
     // Each wave of the workgroup takes its own item and its own LDS slice; the waves never
     // synchronise with each other.  Items are in descending cost order, so the kBwdWaves items of
     // one workgroup cost about the same: grouping them keeps the launch's workgroups coarse, which
@@ -264,6 +264,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     __shared__ float s_park_all[kTred * kTredF * kBwdWaves];  // parked column sums (transposed reduction)
     __shared__ uint32_t s_slot_all[kTred * kBwdWaves];        // staged index j of each parked pair
 #endif
+    if (spec_ok && *spec_ok == 0u) return;  // speculative render half whose forward was redone: redone too
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t item = blockIdx.x * kBwdWaves + wv;
     if (item >= items[0].x) return;  // the launch covers the item bound
@@ -1094,8 +1095,10 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // stream right after k_render_bwd, beside the other views' render kernels.
 constexpr int kSumChunk = 128;
 __global__ __launch_bounds__(256) void k_sum_records(int P, const uint32_t *__restrict__ goff,
-                                                     const float4 *__restrict__ part, float *__restrict__ sums) {
+                                                     const float4 *__restrict__ part, float *__restrict__ sums,
+                                                     const uint32_t *__restrict__ spec_ok) {
     __shared__ float4 s_stage[3 * kSumChunk * 4];
+    if (spec_ok && *spec_ok == 0u) return;  // (as k_render_bwd)
     const int i = blockIdx.x * 256 + threadIdx.x;
     float acc[kPartial];
     sum_records_chunked<kSumChunk>(i, P, goff, part, s_stage + (threadIdx.x >> 6) * 3 * kSumChunk, acc);
@@ -1354,7 +1357,7 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     auto k = a.exact ? k_render_bwd<true> : k_render_bwd<false>;
     k<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
                                                                      a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
-                                                                     a.slot_emit, a.dL_dcolor, a.part, seg_log2(a.P));
+                                                                     a.slot_emit, a.dL_dcolor, a.part, seg_log2(a.P), a.spec_ok);
     return hipGetLastError();
 }
 
@@ -1386,9 +1389,10 @@ static void gauss_bwd_multi_mc(const MultiArgs &a, hipStream_t s) {
     k_gauss_bwd_multi<MC><<<div_up(a.P, kShBlock), kShBlock, multi_lds_bytes<MC>(), s>>>(a);
 }
 
-hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s) {
+hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s,
+                              const uint32_t *spec_ok) {
     if (P == 0) return hipSuccess;
-    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums);
+    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums, spec_ok);
     return hipGetLastError();
 }
 

@@ -59,6 +59,7 @@ struct BwdArgs {
         *dL_drot;
     int accm;  // gsr_grad_bits: outputs accumulated into instead of overwritten
     int exact;  // exact-threshold mode (the forward's)
+    const uint32_t *spec_ok;  // speculative render half (pair count unknown): kernels return when the forward's speculation failed
 };
 
 hipError_t launch_preprocess(const FwdArgs &a, hipStream_t s);
@@ -79,7 +80,8 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 // Each Gaussian's per-pair records of one view summed in emission order into kPartial x P SoA sums
 // (the deferred multi-view pass reads these instead of walking the records itself).
-hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s);
+hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s,
+                              const uint32_t *spec_ok = nullptr);
 
 // Per-Gaussian backward over several views of the same Gaussians (gsr_backward_gaussians): one
 // launch reads the parameters and read-modify-writes every gradient once for up to kMultiViews views.

@@ -186,7 +186,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 18  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 19  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -620,7 +620,10 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
     """The per-pixel half of ``rasterize_gaussians_backward`` (gsr_backward_render): returns the
     view's SUMS byte buffer (each Gaussian's per-(tile, Gaussian) gradient records summed, 9 x P
     floats), for ``rasterize_gaussians_backward_views``; the records' SCRATCH buffer is released here
-    (its last reader is already queued on the current stream)."""
+    (its last reader is already queued on the current stream).  ``R < 0``: the speculative half of an
+    asynchronous forward whose pair count is not known yet (ABI 19): sized for its capacity
+    ``binning_layout`` over its own BINNING; redo it with the resolved values when
+    ``AsyncForward.redone``."""
     L = load_library()
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
@@ -634,7 +637,7 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
     dpix = dL_dout_color.contiguous().float()
     keep.append(dpix)
     # SCRATCH and SUMS as two allocations: SCRATCH is released when this returns, SUMS stays queued
-    alloc = _PreAllocator(dev, [[(GSR_BUF_SCRATCH, L.gsr_scratch_bytes(int(R), W, H))],
+    alloc = _PreAllocator(dev, [[(GSR_BUF_SCRATCH, L.gsr_scratch_bytes(int(R) if R >= 0 else int(binning_layout), W, H))],
                                 [(GSR_BUF_SUMS, L.gsr_sums_bytes(P))]])
     with _device_guard(dev), alloc:
         _check(L.gsr_backward_render(ctypes.byref(cam), ctypes.byref(g), radii.data_ptr(), int(R),

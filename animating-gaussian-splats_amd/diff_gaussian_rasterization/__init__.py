@@ -159,11 +159,16 @@ _defer = {"on": os.environ.get("GSR_DEFER_BACKWARD", "1") != "0",
           # thread per stream (the headline) the host wait for K is already hidden, and the asynchronous
           # bookkeeping cost 1-3 % there; ``async_forward(True)`` / the env switch turn
           # it on for one-thread multi-stream submission (splat_step.RenderStep does)
-          "async": os.environ.get("GSR_ASYNC_FORWARD", "0") == "1"}
+          "async": os.environ.get("GSR_ASYNC_FORWARD", "0") == "1",
+          # a deferred view whose asynchronous forward has no pair count yet queues its render half at
+          # once against the forward's capacity (ABI 19) instead of holding it back to the end of the
+          # pass; the end-of-pass callback only checks the device's verdict and redoes the rare miss
+          "spec_half": os.environ.get("GSR_SPEC_RENDER_HALF", "1") != "0"}
 _async_tls = threading.local()  # async_forward(): a per-thread override of _defer["async"]
 _pending_lock = threading.Lock()
 _pending = {}  # (graph task id, group key) -> {"views": [...], "gauss": (...), "targets": [...], ...}
 _queued = set()  # graph tasks whose flush callback is queued
+_spec_half_stats = {"queued": 0, "redone": 0}  # speculative render halves (diagnostics / tests)
 
 
 def set_deferred_backward(on: bool) -> bool:
@@ -292,7 +297,17 @@ def _run_group(grp, created, post):
     dev = grp["device"]
     with torch.cuda.device(dev):
         cur = torch.cuda.current_stream(dev)
-        for v in grp["views"]:  # render halves held back while their forward's pair count was unknown
+        for v in grp["views"]:
+            pend = v.pop("spec", None)
+            if pend is not None:  # a speculative render half: it stands unless its forward was redone
+                K, _, _ = pend.resolve()
+                if pend.redone:
+                    v["scratch"] = None
+                    _spec_half_stats["redone"] += 1
+                else:
+                    v["num_rendered"] = K
+                    v.pop("render_fn")
+            # render halves held back while their forward's pair count was unknown, or redone
             if v["scratch"] is None:
                 with torch.cuda.stream(v["stream"]):
                     v["scratch"], v["num_rendered"] = v.pop("render_fn")()
@@ -325,11 +340,13 @@ def _run_group(grp, created, post):
 def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_fn, keep=()):
     """Queue this view for the end-of-pass per-Gaussian backward when every gradient it must produce
     can go into a leaf's .grad; returns True when queued (the Function then returns None for all).
-    ``render_fn()`` runs the view's per-pixel half and returns ``(SUMS buffer, num_rendered)``.  When
-    the view's forward was asynchronous and its pair count is not known yet (the GPU has not reached
-    its tile scan -- the pass's first nodes belong to the step's last views), the render half is held
-    back until the end-of-pass callback instead of waiting here, so the earlier views' render halves
-    are queued first."""
+    ``render_fn(spec=False)`` runs the view's per-pixel half and returns ``(SUMS buffer, num_rendered)``.
+    When the view's forward was asynchronous and its pair count is not known yet (the GPU has not
+    reached its tile scan -- the pass's first nodes belong to the step's last views), the half is
+    queued speculatively (``render_fn(True)``: against the forward's capacity, its kernels return at
+    once if the device's speculation failed) and the end-of-pass callback resolves the forward,
+    redoing the half only when the forward was redone; with ``_defer["spec_half"]`` off it is held back
+    until that callback instead, so the earlier views' render halves are queued first."""
     if not _defer["on"]:
         return False
     means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act = gauss
@@ -352,8 +369,13 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
         targets[k] = tgt
     rs = ctx.raster_settings
     stream = torch.cuda.current_stream(means3D.device)
+    spec = None
     if ctx.pending is None or ctx.pending.ready():
         scratch, K = render_fn()
+    elif _defer["spec_half"]:
+        scratch, K = render_fn(True)
+        spec = ctx.pending
+        _spec_half_stats["queued"] += 1
     else:
         scratch, K = None, -1
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else 0  # noqa: E731
@@ -365,8 +387,10 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
             "campos": rs.campos, "bg": rs.bg, "radii": radii, "geomBuffer": geomBuffer, "scratch": scratch,
             "num_rendered": K, "means2D_grad": targets[0], "accumulate_means2D": True, "stream": stream,
             "keep": keep}
-    if scratch is None:
+    if scratch is None or spec is not None:
         view["render_fn"] = render_fn
+    if spec is not None:
+        view["spec"] = spec
     with _pending_lock:
         grp = _pending.get((task, key))
         if grp is None:
@@ -591,15 +615,16 @@ class _RasterizeGaussians(torch.autograd.Function):
         bases = saved[7:]
         geomBuffer, binningBuffer, imgBuffer = ctx.bufs
 
-        def args_kw():  # the forward's pair count and BINNING (an asynchronous forward resolves here)
-            K, layout, bptr = _resolved(ctx)
+        def args_kw(spec=False):  # the forward's pair count and BINNING (an asynchronous forward resolves
+            # here; ``spec``: not yet -- its capacity and own BINNING, the speculative render half)
+            K, layout, bptr = (-1, ctx.binning_layout, None) if spec else _resolved(ctx)
             return ((rs.bg, means3D, radii, colors_precomp, scales, rotations, rs.scale_modifier,
                      cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color,
                      sh, rs.sh_degree, rs.campos, geomBuffer, K, binningBuffer, imgBuffer),
                     {"prepare_backward": ctx.prep, "binning_layout": layout, "binning_ptr": bptr})
 
-        def render_half():
-            a, k = args_kw()
+        def render_half(spec=False):
+            a, k = args_kw(spec)
             return _C.rasterize_gaussians_backward_render(*a, **k), a[17]
         inputs = (1, 3, 4, 0, 7, 2, 5, 6)  # input index of each leaf (grad output order)
         nodes = _input_nodes(ctx, inputs)
@@ -721,8 +746,8 @@ class _RasterizeGaussianParameters(torch.autograd.Function):
         nodes = _input_nodes(ctx, [i for i in inputs if i is not None])
         nodes.insert(4, None)
         gauss = (means, colors, log_scales, quaternions, rs.scale_modifier, empty, sh, rs.sh_degree, _C.ACT_ALL)
-        def render_half():
-            K, layout, bptr = _resolved(ctx)
+        def render_half(spec=False):
+            K, layout, bptr = (-1, ctx.binning_layout, None) if spec else _resolved(ctx)
             return _C.rasterize_gaussians_backward_render(
                 rs.bg, means, radii, colors, log_scales, quaternions, rs.scale_modifier, empty,
                 rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, grad_out_color, sh,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 18
+#define GSR_ABI_VERSION 19
 
 enum gsr_status {
     GSR_OK = 0,
@@ -240,7 +240,16 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
  *
  * The result equals gsr_backward per view with the gradients summed, up to the order of the fp32
  * additions (views are summed in registers, then added to the arrays once).  SH needs M in
- * {1, 4, 9, 16} (GSR_ERR_UNSUPPORTED otherwise). */
+ * {1, 4, 9, 16} (GSR_ERR_UNSUPPORTED otherwise).
+ *
+ * ABI >= 19, speculative render half: gsr_backward_render with num_rendered < 0 and g->binning_layout =
+ * the capacity an asynchronous forward reported (gsr_forward_info.binning_layout) queues the half
+ * before that forward's pair count is known, against its own BINNING buffer, with SCRATCH sized for the
+ * capacity (gsr_scratch_bytes(binning_layout, W, H)).  Its kernels read the device's speculation verdict
+ * and return at once when it failed; the caller then learns `redone` from gsr_forward_resolve and must
+ * call gsr_backward_render again with the resolved num_rendered / binning_layout / BINNING (a fresh
+ * SUMS buffer) before gsr_backward_gaussians.  When the speculation stood the SUMS are final and equal
+ * to those of the resolved call.  gsr_backward rejects num_rendered < 0. */
 typedef struct gsr_view_grad {
     const gsr_camera *cam;   /* the view's camera (as given to its gsr_forward) */
     const int *radii;        /* the view's radii (P) */

@@ -221,3 +221,54 @@ def test_autograd_step_async_equals_blocking(cuda, leaf):
     assert ref[1].keys() == got[1].keys()
     for k in ref[1]:
         assert torch.equal(ref[1][k], got[1][k]), k
+
+
+@pytest.mark.parametrize("miss", [False, True])
+def test_speculative_render_half_bitwise(cuda, miss):
+    """Deferred views whose asynchronous forward is still unresolved when the backward reaches them
+    (the GPU is held busy ahead of the forwards) queue their render half at once against the forward's
+    capacity (ABI 19).  When the speculation stands the half is final; when the forward is redone
+    (``miss``: a denser cloud than the pair-count history, so the capacity is exceeded) its kernels
+    return at once and the end-of-pass callback redoes it.  Images and gradients are bitwise those of
+    blocking forwards either way."""
+    P, W, H = 80_000, 480, 320
+    base = S.synthetic_cloud(P, 0.01, seed=7, device=cuda)
+    cams = [S.render_settings(W, H, S.intrinsics(400.0, W, H), S.look_at(yaw, 0.2, 8.0), device=cuda)
+            for yaw in (0, 72, 144, 216, 288)]
+    dl = S.upstream_grad(H, W, device=cuda)
+    with torch.no_grad():
+        act = S.activated_inputs(base, -1)
+
+    def step(scale, busy):
+        leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
+        with torch.no_grad():
+            leaves["scales"].mul_(scale)
+        if busy:  # the forwards queue behind ~20 ms of device work: none is resolved at the backward
+            torch.cuda._sleep(50_000_000)
+        imgs = [GaussianRasterizer(raster_settings=rs)(**dict(leaves, means2D=torch.zeros_like(
+            leaves["means3D"], requires_grad=True)))[0] for rs in cams]
+        torch.stack([(i * dl).sum() for i in imgs]).sum().backward()
+        torch.cuda.synchronize()
+        return [i.detach() for i in imgs], {k: v.grad for k, v in leaves.items() if v.grad is not None}
+
+    scale = 3.0 if miss else 1.0
+    prev_async, prev_half = dgr.set_async_forward(False), dgr._defer["spec_half"]
+    try:
+        dgr._defer["spec_half"] = True
+        ref = step(scale, False)
+        _C.speculation_stats(reset=True)
+        step(1.0, False)  # pair-count history of the sparse cloud for every view's key
+        dgr.set_async_forward(True)
+        q0, r0 = dgr._spec_half_stats["queued"], dgr._spec_half_stats["redone"]
+        got = step(scale, True)
+        queued, redone = dgr._spec_half_stats["queued"] - q0, dgr._spec_half_stats["redone"] - r0
+    finally:
+        dgr.set_async_forward(prev_async)
+        dgr._defer["spec_half"] = prev_half
+    assert queued > 0
+    assert (redone > 0) == miss, (queued, redone)
+    for x, y in zip(ref[0], got[0]):
+        assert torch.equal(x, y)
+    assert ref[1].keys() == got[1].keys()
+    for k in ref[1]:
+        assert torch.equal(ref[1][k], got[1][k]), k
