@@ -7,8 +7,9 @@ quota, and the kernel scheduler moves the submitting threads onto cores that oth
 C2 ran at 255-460 Msplats/s from one process to the next on one box, and at 479-487 with the process
 pinned to a few idle CPUs of one node (tools/c2_pin.py).  ``pin_host_threads`` picks such CPUs -- the
 least busy ones (sampled from /proc/stat) of the GPU's NUMA node, in this local rank's share of the
-node when several ranks share it -- and pins every thread of the process to them, including the HIP
-runtime's and the library's resolver thread.  Nothing on the device side changes.
+node when several ranks share it, one hardware thread per idle core (a CPU counts as busy as its
+busiest SMT sibling) -- and pins every thread of the process to them, including the HIP runtime's and
+the library's resolver thread.  Nothing on the device side changes.
 """
 from __future__ import annotations
 
@@ -96,6 +97,38 @@ def _busy_fraction(cpus, interval=0.05):
     return busy
 
 
+def _siblings(c):
+    """The SMT siblings of CPU ``c`` (itself included), from sysfs; [c] when unknown."""
+    try:
+        return _cpulist(open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read())
+    except (OSError, ValueError):
+        return [c]
+
+
+def _pick(pool, busy, n, smt):
+    """The ``n`` least busy CPUs of ``pool``.  ``smt``: rank each CPU by the busier of its core's hardware
+    threads (a thread whose sibling runs another tenant's work gets half a core) and take at most one
+    CPU per core while there are enough idle cores, so the process's own threads do not share cores."""
+    if not smt:
+        return sorted(sorted(pool, key=lambda c: (busy.get(c, 1.0), c))[:n])
+    sib = {c: _siblings(c) for c in pool}
+    used = set()
+    # the load on c's core that is not this process's: c and its siblings outside the chosen set
+    foreign = lambda c: max(busy.get(x, 1.0) for x in sib[c] if x == c or x not in used)  # noqa: E731
+    got = []
+    for c in sorted(pool, key=lambda c: (foreign(c), busy.get(c, 1.0), c)):  # one per (nearly) idle core
+        if len(got) == n or foreign(c) > 0.25:
+            break
+        if not used & set(sib[c]):
+            got.append(c)
+            used.add(c)
+    while len(got) < n:  # then the least loaded of the rest (siblings of chosen CPUs count as idle)
+        c = min((c for c in pool if c not in used), key=lambda c: (foreign(c), busy.get(c, 1.0), c))
+        got.append(c)
+        used.add(c)
+    return sorted(got)
+
+
 def choose_cpus(dev_index=0, local_rank=0, local_world=1, n=8):
     """The CPUs ``pin_host_threads`` would use (sorted), or [] when there is no choice to make."""
     if n <= 0 or not hasattr(os, "sched_getaffinity"):
@@ -116,8 +149,11 @@ def choose_cpus(dev_index=0, local_rank=0, local_world=1, n=8):
         start = (local_rank * per) % max(len(pool), 1)
         share = pool[start:start + per]
         pool = share if len(share) >= n else pool
-    busy = _busy_fraction(pool)
-    return sorted(sorted(pool, key=lambda c: (busy.get(c, 1.0), c))[:n])
+    smt = os.environ.get("GSR_PIN_SMT", "1") != "0"
+    # the siblings' load counts too (they may lie outside the pool)
+    busy = _busy_fraction(sorted(set(pool) | {x for c in pool for x in _siblings(c)}) if smt else pool,
+                          float(os.environ.get("GSR_PIN_SAMPLE_S", "0.1")))
+    return _pick(pool, busy, n, smt)
 
 
 def pin_host_threads(dev_index=0, local_rank=0, local_world=1, n=8):

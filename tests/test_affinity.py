@@ -42,3 +42,18 @@ def test_pin_and_unpin_every_thread():
         A.unpin_host_threads(allowed)
         stop.set()
         t.join()
+
+
+def test_pick_prefers_whole_idle_cores():
+    """SMT-aware choice: a CPU whose sibling is busy ranks as busy, and one CPU per core is taken
+    before any sibling pair (sysfs siblings mocked: cores (0, 4), (1, 5), (2, 6), (3, 7))."""
+    sib = {c: sorted({c, c ^ 4}) for c in range(8)}
+    orig = A._siblings
+    A._siblings = lambda c: sib[c]
+    try:
+        busy = {0: 0.0, 4: 0.9, 1: 0.0, 5: 0.0, 2: 0.1, 6: 0.0, 3: 0.0, 7: 0.0}
+        assert A._pick(list(range(8)), busy, 3, smt=True) == [1, 3, 6]  # core (0,4) is busy; one per core
+        assert A._pick(list(range(8)), busy, 3, smt=False) == [0, 1, 3]
+        assert A._pick(list(range(8)), busy, 6, smt=True) == [1, 2, 3, 5, 6, 7]  # siblings once cores run out
+    finally:
+        A._siblings = orig

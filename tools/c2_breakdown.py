@@ -65,7 +65,10 @@ def fwrap(ctx, *a):
 
 dgr._RasterizeGaussians.forward = staticmethod(fwrap)
 dev = torch.device("cuda", 0)
-_C.load_library()
+L = _C.load_library()
+for n in ("gsr_forward_async", "gsr_forward_info_call", "gsr_backward_render", "gsr_backward_gaussians",
+          "gsr_forward_resolve"):  # the C calls themselves (kernel launches + host logic)
+    wrap(L, n, "C." + n)
 torch.zeros(1, device=dev)
 import splat_affinity  # noqa: E402
 print("pinned", splat_affinity.pin_host_threads(0, 0, 1, 8))
