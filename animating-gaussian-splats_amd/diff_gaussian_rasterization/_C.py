@@ -283,14 +283,19 @@ class _PreAllocator:
         _tls.buffers, _tls.device = self.prev
         # what the call took: the pre-allocated buffers it was handed, and the fallback's
         used = self.pa.used
-        self.taken = {w: g for w, g in self.given.items() if (used >> w) & 1}
-        self.fallback = got
-        self.ptrs = {w: self.pa.ptr[w] for w in self.taken}
-        self.ptrs.update({w: t.data_ptr() for w, t in got.items()})
-        bases = {id(g[0]): g[0] for g in self.taken.values()}
-        bases.update({id(t): t for t in got.values()})
-        self.bases = list(bases.values())
+        self._took({w: g for w, g in self.given.items() if (used >> w) & 1}, got)
         return False
+
+    def _took(self, taken, fallback):
+        """``taken``: gsr_buffer -> (base tensor, offset, bytes) of the pre-allocated buffers the call
+        used; ``fallback``: gsr_buffer -> tensor of the requests made through the fallback."""
+        self.taken, self.fallback = taken, fallback
+        self.ptrs = {w: b.data_ptr() + o for w, (b, o, _) in taken.items()}
+        self.ptrs.update({w: t.data_ptr() for w, t in fallback.items()})
+        bases = {id(g[0]): g[0] for g in taken.values()}
+        bases.update({id(t): t for t in fallback.values()})
+        self.bases = list(bases.values())
+        self._views = None
 
     def base_of(self, which):
         """The allocation backing buffer `which` (to record it on another stream)."""
@@ -306,6 +311,43 @@ class _PreAllocator:
             v.update(self.fallback)
             self._views = v
         return self._views
+
+
+class _NativeAlloc(_PreAllocator):
+    """What gsr_bind's calls allocated (their ``(taken, fallback)`` lists), with _PreAllocator's
+    post-call interface (``ptrs``, ``bases``, ``buffers``, ``base_of``)."""
+
+    def __init__(self, res):  # noqa: D107 - no pre-allocation here: gsr_bind made the tensors
+        taken, fallback = res
+        self._took({w: (b, o, n) for w, b, o, n in taken}, dict(fallback))
+
+
+_native_mod = None
+_EMPTY = torch.empty(0)  # an absent tensor argument (gsr_bind treats empty tensors as absent)
+
+
+def _native():
+    """The gsr_bind torch extension (gsr_bind.so next to this file, built by __graft_entry__.build():
+    the two per-view calls' argument marshalling in C++), bound to this process's libgsr; None when it
+    is absent or GSR_NATIVE_BIND=0 -- the ctypes path below does the same work in Python."""
+    global _native_mod
+    if _native_mod is None:
+        _native_mod = False
+        path = os.path.join(_HERE, "gsr_bind.so")
+        if os.environ.get("GSR_NATIVE_BIND", "1") != "0" and os.path.exists(path):
+            import importlib.machinery
+            import importlib.util
+            L = load_library()
+            spec = importlib.util.spec_from_file_location(
+                "gsr_bind", path, loader=importlib.machinery.ExtensionFileLoader("gsr_bind", path))
+            m = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(m)
+            m.set_functions({n: ctypes.cast(getattr(L, n), ctypes.c_void_p).value for n in (
+                "gsr_forward_info_call", "gsr_forward_async", "gsr_backward_render", "gsr_prealloc_alloc",
+                "gsr_spec_binning_bytes", "gsr_geom_bytes", "gsr_image_bytes", "gsr_scratch_bytes",
+                "gsr_sums_bytes", "gsr_last_error")})
+            _native_mod = m
+    return _native_mod or None
 
 
 _get_device = torch._C._cuda_getDevice
@@ -479,6 +521,36 @@ def _forward(background, means3D, colors, opacity, scales, rotations, scale_modi
     """rasterize_gaussians without the buffer views: returns (gsr_forward_info, color, radii, depth,
     the _PreAllocator (``ptrs`` / ``bases`` of GEOM, BINNING, IMAGE), the AsyncForward or None)."""
     L = load_library()
+    nat = _native()
+    if nat is not None:
+        e = _EMPTY
+        (K, layout, spec, pend, aux, color, radii, depth, res) = nat.forward(
+            background, means3D, e if colors is None else colors, e if opacity is None else opacity,
+            e if scales is None else scales,
+            e if rotations is None else rotations, float(scale_modifier), e if cov3D_precomp is None else cov3D_precomp,
+            viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), int(image_height), int(image_width),
+            e if sh is None else sh, int(degree), e if campos is None else campos, bool(prefiltered),
+            int(activations), bool(prepare_backward), bool(speculate), bool(nonblocking), _PREALLOC_ON)
+        fi = _ForwardInfo(K, layout, spec, pend, aux or None)
+        alloc = _NativeAlloc(res)
+    else:
+        fi, color, radii, depth, alloc = _forward_ctypes(
+            L, background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+            projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, activations,
+            prepare_backward, speculate, nonblocking)
+    dev = means3D.device
+    pending = AsyncForward(fi.pending) if fi.pending else None
+    if fi.aux_stream:  # the item list is written into BINNING on the library's auxiliary stream: no early reuse
+        bb = alloc.base_of(GSR_BUF_BINNING)
+        if bb is not None:
+            bb.record_stream(_external_stream(fi.aux_stream, dev))
+    return fi, color, radii, depth, alloc, pending
+
+
+def _forward_ctypes(L, background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                    viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                    prefiltered, activations, prepare_backward, speculate, nonblocking):
+    """_forward's native call over ctypes (without gsr_bind)."""
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, opacity, scales, rotations, scale_modifier,
                          cov3D_precomp, keep, activations, prepare_backward)
@@ -505,12 +577,7 @@ def _forward(background, means3D, colors, opacity, scales, rotations, scale_modi
                 _check(L.gsr_forward_info_call(ctypes.byref(cam), ctypes.byref(g), alloc.cb, alloc.ctx,
                                                color.data_ptr(), depth.data_ptr(), radii.data_ptr() if P else None,
                                                int(bool(speculate)), ctypes.byref(fi), _stream_ptr(dev)))
-    pending = AsyncForward(fi.pending) if fi.pending else None
-    if fi.aux_stream:  # the item list is written into BINNING on the library's auxiliary stream: no early reuse
-        bb = alloc.base_of(GSR_BUF_BINNING)
-        if bb is not None:
-            bb.record_stream(_external_stream(fi.aux_stream, dev))
-    return fi, color, radii, depth, alloc, pending
+    return fi, color, radii, depth, alloc
 
 
 _EXT_STREAMS = {}
@@ -625,6 +692,17 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
     ``binning_layout`` over its own BINNING; redo it with the resolved values when
     ``AsyncForward.redone``."""
     L = load_library()
+    nat = _native()
+    if nat is not None:
+        e = _EMPTY
+        sums, _ = nat.backward_render(
+            background, means3D, radii, e if colors is None else colors, e if scales is None else scales,
+            e if rotations is None else rotations, float(scale_modifier), e if cov3D_precomp is None else cov3D_precomp,
+            viewmatrix, projmatrix, float(tan_fovx), float(tan_fovy), dL_dout_color, e if sh is None else sh,
+            int(degree), e if campos is None else campos, _bp(geomBuffer), int(R),
+            binning_ptr or _bp(binningBuffer), _bp(imageBuffer), int(activations), bool(prepare_backward),
+            int(binning_layout or 0), _PREALLOC_ON)
+        return sums
     keep = []
     g, P, _ = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
                          rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward,
