@@ -4,7 +4,8 @@
 // thread submitting 4 views of 100k Gaussians) most of a call's host time was that Python layer, not
 // the library (per view: forward 58 us of which 26 us in gsr_forward_*, render half 32 us of which
 // 7 us in gsr_backward_render; profiles/r04_c2_host.txt).  This torch extension does the same
-// marshalling in C++ for _C._forward and _C.rasterize_gaussians_backward_render: the argument checks
+// marshalling in C++ for _C._forward, _C.rasterize_gaussians_backward_render and the per-view part of
+// _C.rasterize_gaussians_backward_views: the argument checks
 // (same messages), the camera / Gaussian structs, the output and workspace tensors (the caching
 // allocator, the same pre-allocated groups as _C._PreAllocator) and the call itself, with the
 // interpreter lock released while libgsr runs.  It calls libgsr through the function addresses of the
@@ -12,6 +13,7 @@
 // variants included).  It computes nothing of its own: without it _C.py takes its ctypes path.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <c10/hip/HIPGuard.h>
 
 #include <map>
@@ -29,6 +31,7 @@ struct Fns {
     decltype(&gsr_forward_info_call) forward_info_call = nullptr;
     decltype(&gsr_forward_async) forward_async = nullptr;
     decltype(&gsr_backward_render) backward_render = nullptr;
+    decltype(&gsr_backward_gaussians) backward_gaussians = nullptr;
     decltype(&gsr_prealloc_alloc) prealloc_alloc = nullptr;
     decltype(&gsr_spec_binning_bytes) spec_binning_bytes = nullptr;
     decltype(&gsr_geom_bytes) geom_bytes = nullptr;
@@ -49,6 +52,7 @@ void set_functions(const std::map<std::string, int64_t> &a) {
     take(a, "gsr_forward_info_call", F.forward_info_call);
     take(a, "gsr_forward_async", F.forward_async);
     take(a, "gsr_backward_render", F.backward_render);
+    take(a, "gsr_backward_gaussians", F.backward_gaussians);
     take(a, "gsr_prealloc_alloc", F.prealloc_alloc);
     take(a, "gsr_spec_binning_bytes", F.spec_binning_bytes);
     take(a, "gsr_geom_bytes", F.geom_bytes);
@@ -285,6 +289,85 @@ py::tuple backward_render(const at::Tensor &bg, const at::Tensor &means3D, const
     return py::make_tuple(sums, pa.result());
 }
 
+// Tensor.record_stream(s): the caching allocator keeps t's block from reuse until s's queued work is done
+void record(const at::Tensor &t, const c10::hip::HIPStream &s) {
+    if (t.defined() && t.is_cuda() && t.storage().data_ptr().get())
+        c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), s);
+}
+
+std::string dev_str(const at::Device &d) { return d.str(); }
+
+// _C.rasterize_gaussians_backward_views after its output allocation: `views` are the deferred views'
+// dicts, `outs` the 8 gradient tensors (or None) with their accumulate bits
+void backward_views(const py::list &views, const at::Tensor &means3D, const at::Tensor &colors,
+                    const at::Tensor &scales, const at::Tensor &rotations, double scale_modifier, const at::Tensor &cov3D,
+                    const at::Tensor &sh, int degree, int activations, const std::vector<c10::optional<at::Tensor>> &outs,
+                    int acc_bits) {
+    std::vector<at::Tensor> keep;
+    gsr_gaussians g = gaussians(means3D, sh, degree, colors, at::Tensor(), scales, rotations, scale_modifier, cov3D,
+                                activations, false, 0, keep);
+    const int P = g.P;
+    const int nv = (int)views.size();
+    if (P == 0 || nv == 0) return;
+    const at::Device dev = means3D.device();
+    c10::hip::HIPGuard guard(dev.index());
+    const c10::hip::HIPStream cs = c10::hip::getCurrentHIPStream(dev.index());
+    std::vector<gsr_camera> cams(nv);
+    std::vector<gsr_view_grad> vg(nv);
+    for (int k = 0; k < nv; ++k) {
+        const py::dict v = views[k].cast<py::dict>();
+        cams[k] = camera(v["viewmatrix"].cast<at::Tensor>(), v["projmatrix"].cast<at::Tensor>(),
+                         v["tanfovx"].cast<double>(), v["tanfovy"].cast<double>(), v["image_height"].cast<int>(),
+                         v["image_width"].cast<int>(),
+                         v["campos"].is_none() ? at::Tensor() : v["campos"].cast<at::Tensor>(),
+                         v["bg"].cast<at::Tensor>(), false, keep);
+        float *m2p = nullptr;
+        if (v.contains("means2D_grad") && !v["means2D_grad"].is_none()) {
+            const at::Tensor m2 = v["means2D_grad"].cast<at::Tensor>();
+            if (m2.dim() != 2 || m2.size(0) != P || m2.size(1) != 3 || m2.scalar_type() != at::kFloat ||
+                !m2.is_contiguous() || m2.device() != dev)
+                throw std::runtime_error("views[" + std::to_string(k) + "]['means2D_grad']: expected a contiguous float32 (" +
+                                         std::to_string(P) + ", 3) tensor on " + dev_str(dev));
+            record(m2, cs);
+            m2p = m2.data_ptr<float>();
+        }
+        const at::Tensor radii = v["radii"].cast<at::Tensor>(), scratch = v["scratch"].cast<at::Tensor>();
+        record(radii, cs);
+        record(scratch, cs);
+        if (v.contains("keep"))
+            for (auto h : v["keep"]) record(h.cast<at::Tensor>(), cs);
+        const py::object gb = v["geomBuffer"];
+        const void *geom;
+        if (py::isinstance<py::int_>(gb)) geom = (const void *)gb.cast<int64_t>();
+        else {
+            const at::Tensor gt = gb.cast<at::Tensor>();
+            record(gt, cs);
+            geom = gt.data_ptr();
+        }
+        vg[k].cam = &cams[k];
+        vg[k].radii = radii.data_ptr<int>();
+        vg[k].geom = geom;
+        vg[k].scratch = scratch.data_ptr();
+        vg[k].num_rendered = v["num_rendered"].cast<int>();
+        vg[k].dL_dmeans2D = m2p;
+        vg[k].accumulate_means2D = (v.contains("accumulate_means2D") && v["accumulate_means2D"].cast<bool>()) ? 1 : 0;
+    }
+    gsr_grads gr;
+    memset(&gr, 0, sizeof(gr));
+    float **slot[8] = {&gr.dL_dmeans2D, &gr.dL_dcolors, &gr.dL_dopacity, &gr.dL_dmeans3D,
+                       &gr.dL_dcov3D, &gr.dL_dsh, &gr.dL_dscales, &gr.dL_drotations};
+    for (int k = 0; k < 8 && k < (int)outs.size(); ++k)
+        if (outs[k].has_value() && present(*outs[k])) *slot[k] = outs[k]->data_ptr<float>();
+    gr.accumulate = acc_bits;
+    void *s = (void *)cs.stream();
+    int rc;
+    {
+        py::gil_scoped_release nogil;
+        rc = F.backward_gaussians(nv, vg.data(), &g, &gr, s);
+    }
+    check(rc);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -292,4 +375,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("set_functions", &set_functions);
     m.def("forward", &forward);
     m.def("backward_render", &backward_render);
+    m.def("backward_views", &backward_views);
 }

@@ -323,6 +323,8 @@ class _NativeAlloc(_PreAllocator):
 
 
 _native_mod = None
+# GSR_NATIVE_BIND: bit mask of the calls gsr_bind takes over (1 forward, 2 render half, 4 views; 0 none)
+_NATIVE_PARTS = int(os.environ.get("GSR_NATIVE_BIND", "7"))
 _EMPTY = torch.empty(0)  # an absent tensor argument (gsr_bind treats empty tensors as absent)
 
 
@@ -334,7 +336,7 @@ def _native():
     if _native_mod is None:
         _native_mod = False
         path = os.path.join(_HERE, "gsr_bind.so")
-        if os.environ.get("GSR_NATIVE_BIND", "1") != "0" and os.path.exists(path):
+        if _NATIVE_PARTS and os.path.exists(path):
             import importlib.machinery
             import importlib.util
             L = load_library()
@@ -342,8 +344,9 @@ def _native():
                 "gsr_bind", path, loader=importlib.machinery.ExtensionFileLoader("gsr_bind", path))
             m = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(m)
-            m.set_functions({n: ctypes.cast(getattr(L, n), ctypes.c_void_p).value for n in (
-                "gsr_forward_info_call", "gsr_forward_async", "gsr_backward_render", "gsr_prealloc_alloc",
+            m.set_functions({n: ctypes.cast(L[n], ctypes.c_void_p).value for n in (  # (L[n]: the symbol itself)
+                "gsr_forward_info_call", "gsr_forward_async", "gsr_backward_render", "gsr_backward_gaussians",
+                "gsr_prealloc_alloc",
                 "gsr_spec_binning_bytes", "gsr_geom_bytes", "gsr_image_bytes", "gsr_scratch_bytes",
                 "gsr_sums_bytes", "gsr_last_error")})
             _native_mod = m
@@ -521,7 +524,7 @@ def _forward(background, means3D, colors, opacity, scales, rotations, scale_modi
     """rasterize_gaussians without the buffer views: returns (gsr_forward_info, color, radii, depth,
     the _PreAllocator (``ptrs`` / ``bases`` of GEOM, BINNING, IMAGE), the AsyncForward or None)."""
     L = load_library()
-    nat = _native()
+    nat = _native() if _NATIVE_PARTS & 1 else None
     if nat is not None:
         e = _EMPTY
         (K, layout, spec, pend, aux, color, radii, depth, res) = nat.forward(
@@ -692,7 +695,7 @@ def rasterize_gaussians_backward_render(background, means3D, radii, colors, scal
     ``binning_layout`` over its own BINNING; redo it with the resolved values when
     ``AsyncForward.redone``."""
     L = load_library()
-    nat = _native()
+    nat = _native() if _NATIVE_PARTS & 2 else None
     if nat is not None:
         e = _EMPTY
         sums, _ = nat.backward_render(
@@ -748,6 +751,14 @@ def rasterize_gaussians_backward_views(views, means3D, colors, scales, rotations
     out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
                                   accumulate_into, skip=skip, overwrite=overwrite)
     if P == 0 or not views:
+        return out
+    nat = _native() if _NATIVE_PARTS & 4 else None
+    if nat is not None:
+        e = _EMPTY
+        nat.backward_views(list(views), means3D, e if colors is None else colors, e if scales is None else scales,
+                           e if rotations is None else rotations, float(scale_modifier),
+                           e if cov3D_precomp is None else cov3D_precomp, e if sh is None else sh, int(degree),
+                           int(activations), list(out), int(acc_bits))
         return out
     cams = []
     vg = (_ViewGrad * len(views))()

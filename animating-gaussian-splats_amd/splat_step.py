@@ -47,11 +47,17 @@ class RenderStep:
         self.shape = shape
         self.rotate = os.environ.get("GSR_STREAM_ROTATE", "1") != "0" if rotate is None else rotate
         self.calls = 0
-        self.pool = ThreadPoolExecutor(max_workers=len(self.streams)) if threads and len(self.streams) > 1 else None
+        # one single-thread executor per stream: a stream's views are always submitted by the same
+        # thread, so the autograd nodes' sequence numbers (per-thread counters) and with them the order
+        # in which the backward visits the views -- the order the deferred multi-view pass sums them in,
+        # as AccumulateGrad would -- do not depend on which idle pool thread took which task
+        self.pool = ([ThreadPoolExecutor(max_workers=1) for _ in self.streams]
+                     if threads and len(self.streams) > 1 else None)
 
     def close(self):
         if self.pool is not None:
-            self.pool.shutdown()
+            for ex in self.pool:
+                ex.shutdown()
             self.pool = None
 
     def _forwards(self, vs, s):  # one stream's share of a summed step's forwards
@@ -81,7 +87,8 @@ class RenderStep:
     def _run(self, views, ns, pool, streams):
         if self.shape == "summed":
             if pool is not None:
-                futs = [pool.submit(self._forwards, views[k::ns], streams[k]) for k in range(min(ns, len(views)))]
+                futs = [pool[self.streams.index(streams[k])].submit(self._forwards, views[k::ns], streams[k])
+                        for k in range(min(ns, len(views)))]
                 imgs = [None] * len(views)
                 for k, f in enumerate(futs):
                     imgs[k::ns] = f.result()
@@ -92,7 +99,8 @@ class RenderStep:
             torch.autograd.backward(imgs, [self.dl] * len(imgs))
             return [img.detach() for img in imgs]
         elif pool is not None:
-            futs = [pool.submit(self._fwd_bwd, views[k::ns], streams[k]) for k in range(min(ns, len(views)))]
+            futs = [pool[self.streams.index(streams[k])].submit(self._fwd_bwd, views[k::ns], streams[k])
+                    for k in range(min(ns, len(views)))]
             for f in futs:
                 f.result()
         else:
