@@ -92,10 +92,16 @@ class RenderStep:
                 imgs = [None] * len(views)
                 for k, f in enumerate(futs):
                     imgs[k::ns] = f.result()
-            else:
+            else:  # one submitting thread: the device once, the stream switched per view and restored
                 imgs = []
-                for k, ci in enumerate(views):
-                    imgs += self._forwards([ci], streams[k % ns])
+                torch.cuda.set_device(self.device)
+                cur = torch.cuda.current_stream(self.device)
+                try:
+                    for k, ci in enumerate(views):
+                        torch.cuda.set_stream(streams[k % ns])
+                        imgs.append(GaussianRasterizer(raster_settings=self.cams[ci])(**self.inputs_of(ci))[0])
+                finally:
+                    torch.cuda.set_stream(cur)
             torch.autograd.backward(imgs, [self.dl] * len(imgs))
             return [img.detach() for img in imgs]
         elif pool is not None:
