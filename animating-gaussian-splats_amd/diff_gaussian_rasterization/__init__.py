@@ -309,11 +309,12 @@ def _run_group(grp, created, post):
                     v.pop("render_fn")
             # render halves held back while their forward's pair count was unknown, or redone
             if v["scratch"] is None:
-                with torch.cuda.stream(v["stream"]):
+                with torch.cuda.stream(_C._external_stream(v["stream"], dev)):
                     v["scratch"], v["num_rendered"] = v.pop("render_fn")()
+        cur_ptr = cur.cuda_stream
         for s in grp["streams"]:  # every view's render half precedes the per-Gaussian pass
-            if s != cur:
-                cur.wait_stream(s)
+            if s != cur_ptr:
+                cur.wait_stream(_C._external_stream(s, dev))
         (means3D, colors, scales, rotations, scale_modifier, cov3D, sh, degree, act) = grp["gauss"]
         targets, over = [None] * 8, []
         for k in range(1, 8):
@@ -368,7 +369,9 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
             return False  # autograd must receive this gradient: immediate path
         targets[k] = tgt
     rs = ctx.raster_settings
-    stream = torch.cuda.current_stream(means3D.device)
+    # the view's stream as its raw handle (torch.cuda.current_stream builds a Stream object per call)
+    dix = means3D.device.index
+    stream = _C._raw_stream(dix if dix is not None else _C._get_device())
     spec = None
     if ctx.pending is None or ctx.pending.ready():
         scratch, K = render_fn()
