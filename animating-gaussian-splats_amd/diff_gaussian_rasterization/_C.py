@@ -343,7 +343,12 @@ def _native():
             spec = importlib.util.spec_from_file_location(
                 "gsr_bind", path, loader=importlib.machinery.ExtensionFileLoader("gsr_bind", path))
             m = importlib.util.module_from_spec(spec)
-            spec.loader.exec_module(m)
+            try:
+                spec.loader.exec_module(m)
+            except ImportError as err:  # a stale build (another torch): the ctypes marshalling, same kernels
+                import warnings
+                warnings.warn(f"gsr_bind.so not loadable ({err}); binding libgsr through ctypes instead")
+                return None
             m.set_functions({n: ctypes.cast(L[n], ctypes.c_void_p).value for n in (  # (L[n]: the symbol itself)
                 "gsr_forward_info_call", "gsr_forward_async", "gsr_backward_render", "gsr_backward_gaussians",
                 "gsr_prealloc_alloc",
