@@ -4,7 +4,8 @@
 // thread submitting 4 views of 100k Gaussians) most of a call's host time was that Python layer, not
 // the library (per view: forward 58 us of which 26 us in gsr_forward_*, render half 32 us of which
 // 7 us in gsr_backward_render; profiles/r04_c2_host.txt).  This torch extension does the same
-// marshalling in C++ for _C._forward, _C.rasterize_gaussians_backward_render and the per-view part of
+// marshalling in C++ for _C._forward, _C.rasterize_gaussians_backward (after its output allocation),
+// _C.rasterize_gaussians_backward_render and the per-view part of
 // _C.rasterize_gaussians_backward_views: the argument checks
 // (same messages), the camera / Gaussian structs, the output and workspace tensors (the caching
 // allocator, the same pre-allocated groups as _C._PreAllocator) and the call itself, with the
@@ -32,6 +33,7 @@ struct Fns {
     decltype(&gsr_forward_async) forward_async = nullptr;
     decltype(&gsr_backward_render) backward_render = nullptr;
     decltype(&gsr_backward_gaussians) backward_gaussians = nullptr;
+    decltype(&gsr_backward) backward = nullptr;
     decltype(&gsr_prealloc_alloc) prealloc_alloc = nullptr;
     decltype(&gsr_spec_binning_bytes) spec_binning_bytes = nullptr;
     decltype(&gsr_geom_bytes) geom_bytes = nullptr;
@@ -53,6 +55,7 @@ void set_functions(const std::map<std::string, int64_t> &a) {
     take(a, "gsr_forward_async", F.forward_async);
     take(a, "gsr_backward_render", F.backward_render);
     take(a, "gsr_backward_gaussians", F.backward_gaussians);
+    take(a, "gsr_backward", F.backward);
     take(a, "gsr_prealloc_alloc", F.prealloc_alloc);
     take(a, "gsr_spec_binning_bytes", F.spec_binning_bytes);
     take(a, "gsr_geom_bytes", F.geom_bytes);
@@ -289,6 +292,47 @@ py::tuple backward_render(const at::Tensor &bg, const at::Tensor &means3D, const
     return py::make_tuple(sums, pa.result());
 }
 
+void fill_grads(gsr_grads &gr, const std::vector<c10::optional<at::Tensor>> &outs, int acc_bits) {
+    memset(&gr, 0, sizeof(gr));
+    float **slot[8] = {&gr.dL_dmeans2D, &gr.dL_dcolors, &gr.dL_dopacity, &gr.dL_dmeans3D,
+                       &gr.dL_dcov3D, &gr.dL_dsh, &gr.dL_dscales, &gr.dL_drotations};
+    for (int k = 0; k < 8 && k < (int)outs.size(); ++k)
+        if (outs[k].has_value() && present(*outs[k])) *slot[k] = outs[k]->data_ptr<float>();
+    gr.accumulate = acc_bits;
+}
+
+// _C.rasterize_gaussians_backward after its output allocation (`outs`: the 8 gradients or None, their
+// accumulate bits): the one-call backward of one view
+void backward(const at::Tensor &bg, const at::Tensor &means3D, const at::Tensor &radii, const at::Tensor &colors,
+              const at::Tensor &scales, const at::Tensor &rotations, double scale_modifier, const at::Tensor &cov3D,
+              const at::Tensor &viewmatrix, const at::Tensor &projmatrix, double tanfovx, double tanfovy,
+              const at::Tensor &dL_dcolor, const at::Tensor &sh, int degree, const at::Tensor &campos, int64_t geom,
+              int R, int64_t binning, int64_t image, int activations, bool prepare_backward, int binning_layout,
+              const std::vector<c10::optional<at::Tensor>> &outs, int acc_bits, bool prealloc) {
+    std::vector<at::Tensor> keep;
+    gsr_gaussians g = gaussians(means3D, sh, degree, colors, at::Tensor(), scales, rotations, scale_modifier, cov3D,
+                                activations, prepare_backward, binning_layout, keep);
+    const int H = (int)dL_dcolor.size(-2), W = (int)dL_dcolor.size(-1);
+    gsr_camera cam = camera(viewmatrix, projmatrix, tanfovx, tanfovy, H, W, campos, bg, false, keep);
+    if (g.P == 0) return;
+    const at::Device dev = means3D.device();
+    at::Tensor dpix = dL_dcolor.contiguous().to(at::kFloat);
+    c10::hip::HIPGuard guard(dev.index());
+    PreAlloc pa(dev);
+    pa.group({{GSR_BUF_SCRATCH, F.scratch_bytes(R, W, H)}}, prealloc);
+    pa.arm();
+    gsr_grads gr;
+    fill_grads(gr, outs, acc_bits);
+    void *s = raw_stream(dev);
+    int rc;
+    {
+        py::gil_scoped_release nogil;
+        rc = F.backward(&cam, &g, radii.data_ptr<int>(), R, (const void *)geom, (const void *)binning,
+                        (const void *)image, dpix.data_ptr<float>(), nullptr, F.prealloc_alloc, &pa.pa, &gr, s);
+    }
+    check(rc);
+}
+
 // Tensor.record_stream(s): the caching allocator keeps t's block from reuse until s's queued work is done
 void record(const at::Tensor &t, const c10::hip::HIPStream &s) {
     if (t.defined() && t.is_cuda() && t.storage().data_ptr().get())
@@ -353,12 +397,7 @@ void backward_views(const py::list &views, const at::Tensor &means3D, const at::
         vg[k].accumulate_means2D = (v.contains("accumulate_means2D") && v["accumulate_means2D"].cast<bool>()) ? 1 : 0;
     }
     gsr_grads gr;
-    memset(&gr, 0, sizeof(gr));
-    float **slot[8] = {&gr.dL_dmeans2D, &gr.dL_dcolors, &gr.dL_dopacity, &gr.dL_dmeans3D,
-                       &gr.dL_dcov3D, &gr.dL_dsh, &gr.dL_dscales, &gr.dL_drotations};
-    for (int k = 0; k < 8 && k < (int)outs.size(); ++k)
-        if (outs[k].has_value() && present(*outs[k])) *slot[k] = outs[k]->data_ptr<float>();
-    gr.accumulate = acc_bits;
+    fill_grads(gr, outs, acc_bits);
     void *s = (void *)cs.stream();
     int rc;
     {
@@ -376,4 +415,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("forward", &forward);
     m.def("backward_render", &backward_render);
     m.def("backward_views", &backward_views);
+    m.def("backward", &backward);
 }

@@ -323,8 +323,9 @@ class _NativeAlloc(_PreAllocator):
 
 
 _native_mod = None
-# GSR_NATIVE_BIND: bit mask of the calls gsr_bind takes over (1 forward, 2 render half, 4 views; 0 none)
-_NATIVE_PARTS = int(os.environ.get("GSR_NATIVE_BIND", "7"))
+# GSR_NATIVE_BIND: bit mask of the calls gsr_bind takes over (1 forward, 2 render half, 4 views,
+# 8 one-call backward; 0 none)
+_NATIVE_PARTS = int(os.environ.get("GSR_NATIVE_BIND", "15"))
 _EMPTY = torch.empty(0)  # an absent tensor argument (gsr_bind treats empty tensors as absent)
 
 
@@ -351,7 +352,7 @@ def _native():
                 return None
             m.set_functions({n: ctypes.cast(L[n], ctypes.c_void_p).value for n in (  # (L[n]: the symbol itself)
                 "gsr_forward_info_call", "gsr_forward_async", "gsr_backward_render", "gsr_backward_gaussians",
-                "gsr_prealloc_alloc",
+                "gsr_backward", "gsr_prealloc_alloc",
                 "gsr_spec_binning_bytes", "gsr_geom_bytes", "gsr_image_bytes", "gsr_scratch_bytes",
                 "gsr_sums_bytes", "gsr_last_error")})
             _native_mod = m
@@ -664,6 +665,24 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     rotations and means2D need a gradient there).  ``binning_ptr``: the BINNING buffer to read instead
     of ``binningBuffer``'s (an asynchronous forward's, from ``AsyncForward.resolve()``)."""
     L = load_library()
+    nat = _native() if _NATIVE_PARTS & 8 else None
+    if nat is not None:
+        if means3D.ndimension() != 2 or means3D.size(1) != 3:
+            raise RuntimeError("means3D must have dimensions (num_points, 3)")
+        P, dev = means3D.size(0), means3D.device
+        M = sh.size(1) if sh is not None and sh.numel() else 0
+        skip = tuple(k for k in range(8) if needed is not None and not needed[k])
+        out, acc_bits = _grad_outputs(P, M, dev, colors, cov3D_precomp, scales, rotations, skip_unused,
+                                      accumulate_into, skip=skip)
+        e = _EMPTY
+        nat.backward(background, means3D, radii, e if colors is None else colors, e if scales is None else scales,
+                     e if rotations is None else rotations, float(scale_modifier),
+                     e if cov3D_precomp is None else cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx),
+                     float(tan_fovy), dL_dout_color, e if sh is None else sh, int(degree),
+                     e if campos is None else campos, _bp(geomBuffer), int(R), binning_ptr or _bp(binningBuffer),
+                     _bp(imageBuffer), int(activations), bool(prepare_backward), int(binning_layout or 0),
+                     list(out), int(acc_bits), _PREALLOC_ON)
+        return out
     keep = []
     g, P, M = _gaussians(means3D, sh, degree, colors, torch.empty(0, device=means3D.device), scales,
                          rotations, scale_modifier, cov3D_precomp, keep, activations, prepare_backward,

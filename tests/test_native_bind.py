@@ -56,10 +56,10 @@ def test_native_equals_ctypes(cuda, parts, leaf, sh_degree):
                               sh_degree=max(sh_degree, 0)) for yaw in (0, 90, 180)]
     dl = S.upstream_grad(H, W, device=cuda)
     out = {}
-    for mode in (0, 7, 0, 7):  # twice each: the second pass of a mode speculates from the history
+    for mode in (0, 15, 0, 15):  # twice each: the second pass of a mode speculates from the history
         _C._NATIVE_PARTS = mode
         out.setdefault(mode, []).append(_summed_step(cfg, cams, act, dl, cuda, leaf))
-    for a, b in zip(out[0], out[7]):
+    for a, b in zip(out[0], out[15]):
         for x, y in zip(a[0], b[0]):
             assert torch.equal(x, y)
         assert a[1].keys() == b[1].keys()
@@ -84,7 +84,7 @@ def test_native_error_texts(cuda, parts):
              dict(scales=a["scales"].cpu())]
     for over in cases:
         msgs = []
-        for mode in (0, 7):
+        for mode in (0, 15):
             _C._NATIVE_PARTS = mode
             with pytest.raises(RuntimeError) as ei:
                 call(**over)

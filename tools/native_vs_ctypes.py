@@ -19,7 +19,7 @@ e = torch.empty(0, device=cuda)
 
 
 def fwd(rs, mode, spec):
-    _C._NATIVE_PARTS = 7 if mode == "nat" else 0
+    _C._NATIVE_PARTS = 15 if mode == "nat" else 0
     info = {}
     out = _C.rasterize_gaussians(rs.bg, a["means3D"], a["colors_precomp"], a["opacities"], a["scales"], a["rotations"],
                                  1.0, e, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
