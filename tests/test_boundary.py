@@ -130,3 +130,14 @@ def test_rasterizer_validation_and_no_cpu_path():
     with pytest.raises(RuntimeError, match=r"means3D must have dimensions \(num_points, 3\)"):
         r(means3D=torch.zeros(4, 2), means2D=m, opacities=torch.ones(4, 1), colors_precomp=m, scales=m,
           rotations=torch.zeros(4, 4))
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(_C.__file__), "gsr_bind.so")),
+                    reason="gsr_bind.so not built")
+def test_native_marshalling_module_loads():
+    """gsr_bind (the C++ marshalling of the per-call bindings) loads against this torch and takes the
+    library's symbol addresses -- no GPU call."""
+    m = _C._native()
+    assert m is not None
+    for name in ("forward", "backward", "backward_render", "backward_views", "set_functions"):
+        assert hasattr(m, name), name
