@@ -36,7 +36,7 @@ def wrap(mod, name, tag):
 for n in ("_forward", "rasterize_gaussians_backward_render", "rasterize_gaussians_backward_views", "_gaussians",
           "_camera"):
     wrap(_C, n, "_C." + n)
-for n in ("_try_defer", "_flush_pending", "_run_group"):
+for n in ("_try_defer", "_flush_pending", "_run_group", "_accumulation_target", "_fresh_target", "_input_nodes"):
     wrap(dgr, n, "dgr." + n)
 bw = dgr._RasterizeGaussians.backward
 
