@@ -370,81 +370,6 @@ void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome, u
     if (outcome < 0) ++g_spec_misses;
 }
 
-// ---- the backward's item list on an auxiliary stream (ABI 17) ---------------------------------
-// k_bwd_items is one 1024-thread block (~30 us alone) that only the backward reads.  On the caller's
-// stream it sits between the forward's render and whatever the caller queues next (train.py: the
-// view's loss, the next view's activations and forward), with the rest of the chip idle.  The forward
-// therefore queues it on a per-device library stream, forked from the caller's stream by an event
-// after the render; the backward's render half waits for it (items_join) before k_render_bwd.  The
-// caller keeps the BINNING buffer from being reused before the auxiliary stream is done with it
-// (gsr_forward_info.aux_stream: torch's record_stream on an ExternalStream of it).
-// Off by default (GSR_ITEMS_AUX=1 turns it on): with the item kernel's per-wave reservations it is
-// short, and on the auxiliary stream it cost the 3-stream headline step 4-5 % (an extra stream competing
-// for the chip, the cross-stream event per view).
-bool g_items_aux = [] {
-    const char *e = getenv("GSR_ITEMS_AUX");
-    return e && e[0] == '1';
-}();
-std::mutex g_items_mu;
-std::map<int, hipStream_t> g_aux;                       // device -> auxiliary stream
-std::unordered_map<const void *, hipEvent_t> g_items;  // item list -> event after its k_bwd_items
-std::vector<hipEvent_t> g_items_evpool;
-
-hipEvent_t items_event() {  // (g_items_mu held)
-    if (!g_items_evpool.empty()) { hipEvent_t e = g_items_evpool.back(); g_items_evpool.pop_back(); return e; }
-    hipEvent_t e = nullptr;
-    return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess ? e : nullptr;
-}
-
-hipStream_t aux_stream(int dev) {  // (g_items_mu held)
-    hipStream_t &a = g_aux[dev];
-    if (!a && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) a = nullptr;
-    return a;
-}
-
-// Queue the item list of `items` (launch(stream)) on the auxiliary stream after the work queued so far on
-// `s`; returns the auxiliary stream, or nullptr when it ran on `s` itself.
-template <typename Launch>
-hipError_t items_fork(int dev, hipStream_t s, const void *items, Launch launch, hipStream_t *used) {
-    *used = nullptr;
-    std::lock_guard<std::mutex> lk(g_items_mu);
-    hipStream_t aux = g_items_aux ? aux_stream(dev) : nullptr;
-    hipEvent_t fork = aux ? items_event() : nullptr, join = aux ? items_event() : nullptr;
-    if (!aux || !fork || !join) {
-        if (fork) g_items_evpool.push_back(fork);
-        if (join) g_items_evpool.push_back(join);
-        return launch(s);
-    }
-    hipError_t r = hipEventRecord(fork, s);
-    if (r == hipSuccess) r = hipStreamWaitEvent(aux, fork, 0);
-    if (r == hipSuccess) r = launch(aux);
-    if (r == hipSuccess) r = hipEventRecord(join, aux);
-    g_items_evpool.push_back(fork);  // a pending record may be re-recorded: the wait above is queued
-    if (r != hipSuccess) { g_items_evpool.push_back(join); return r; }
-    auto it = g_items.find(items);
-    if (it != g_items.end()) g_items_evpool.push_back(it->second);
-    g_items[items] = join;
-    if (g_items.size() > 256) {  // forwards whose backward never came: drop finished entries
-        for (auto e = g_items.begin(); e != g_items.end();)
-            if (hipEventQuery(e->second) == hipSuccess) { g_items_evpool.push_back(e->second); e = g_items.erase(e); }
-            else ++e;
-    }
-    *used = aux;
-    return hipSuccess;
-}
-
-// The backward's stream waits for the item list at `items` when the forward built it on the
-// auxiliary stream.
-hipError_t items_join(const void *items, hipStream_t s) {
-    std::lock_guard<std::mutex> lk(g_items_mu);
-    auto it = g_items.find(items);
-    if (it == g_items.end()) return hipSuccess;
-    const hipError_t r = hipStreamWaitEvent(s, it->second, 0);
-    g_items_evpool.push_back(it->second);
-    g_items.erase(it);
-    return r;
-}
-
 // ---- asynchronous forwards (ABI 17, gsr_forward_async) ------------------------------------------
 // A speculative forward whose capacity came from the key's history returns as soon as its kernels are
 // queued, without reading num_rendered back.  Each such forward takes a slot of a host-mapped ring:
@@ -792,12 +717,8 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(sa, s)); }
         if (GSR_FWD_ITEMS && g->prepare_backward) {
             uint2 *items = (uint2 *)(spec_bin + BinningLayout((int)cap, a.P).total);
-            hipStream_t used = nullptr;
-            HIP_TRY(items_fork(dev, s, items, [&](hipStream_t q) {
-                Phase ph(q, "bwd_items");
-                return launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, q, sa.spec_ok);
-            }, &used));
-            info->aux_stream = used;
+            Phase ph(s, "bwd_items");
+            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, s, sa.spec_ok));
         }
     }
     if (af) {  // asynchronous: gate the stream on the verdict and return
@@ -866,12 +787,8 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // the backward's item list, built here, off its critical path
         uint2 *items = (uint2 *)(bin + bin_bytes);
-        hipStream_t used = nullptr;
-        HIP_TRY(items_fork(dev, s, items, [&](hipStream_t q) {
-            Phase ph(q, "bwd_items");
-            return launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, q);
-        }, &used));
-        if (used) info->aux_stream = used;
+        Phase ph(s, "bwd_items");
+        HIP_TRY(launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, s));
     }
     info->binning_layout = (int)K;
     spec_record(key, K, n_vlong > 0, cap ? -1 : 0, n_mid);
@@ -1061,7 +978,6 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
     if (GSR_FWD_ITEMS && g->prepare_backward) {  // built by the forward, after the binning arrays
         a.items = (uint2 *)((char *)binning + BinningLayout(layout, a.P).total);
-        HIP_TRY(items_join(a.items, s));  // (queued on the auxiliary stream)
     } else {
         a.items = (uint2 *)(scr + SL.items);
         Phase ph(s, "bwd_items");

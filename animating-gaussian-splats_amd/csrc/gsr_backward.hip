@@ -133,7 +133,8 @@ __global__ __launch_bounds__(kItemsBlock) void k_items_count(int T, const uint2 
         if (h) atomicAdd(&ws[b], h);
     }
     // (no agent-scope fence: it would write back / invalidate the XCD's whole L2; the counts are
-    // device-scope atomics, drained by the workgroup-scope fence's vmcnt wait)
+    // device-scope atomics, drained by an explicit vmcnt(0) before the done counter)
+    drain_vmem();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) s_last = atomicAdd(&ws[2 * kOrderBuckets], 1u) == gridDim.x - 1 ? 1u : 0u;
@@ -188,10 +189,10 @@ __global__ __launch_bounds__(kItemsBlock) void k_items_emit(int T, const uint2 *
 
 // One wave64 per (tile, segment) item, 4 pixels per lane (pixel k of lane l: column l & 15, row
 // (l >> 4) + 4 k, i.e. quarter k = rows 4k..4k+3), reverse walk over the segment's entries in
-// batches of 64.  Per surviving (tile, Gaussian) pair each contributing pixel adds s = dL/dG * G
-// times (dx, dy, dx^2, dx dy, dy^2) plus dL/dopacity and dL/dcolour terms; the lane sums its 4
-// pixels in registers, the wave reduces them with permlane swaps + DPP (wave_pair_sums), and at the
-// end of the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
+// batches of 64.  Per surviving (tile, Gaussian) pair each contributing pixel adds sG = o G dL/dalpha
+// times (1, dx, dy, dx^2, dx dy, dy^2) and w dL/dpix (w = alpha T, the colour gradient); the lane
+// sums its 4 pixels in registers, the wave reduces them with permlane swaps + DPP (pair_sums), and at
+// the end of the batch the lane that staged Gaussian j turns its sums into the reference's per-pair
 // quantities (dmeans2D in NDC units, dconic (a, b, c) in the b/2 convention, dopacity, dcolour) with
 // the exact conic, storing one 36-byte record at the pair's emission slot (no atomics).
 //
@@ -212,37 +213,143 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
 }
 
 #ifndef GSR_BWD_WPE
-#define GSR_BWD_WPE 5  // waves per SIMD the register budget is held to (0: compiler's choice)
+#define GSR_BWD_WPE 5  // waves per SIMD the register budget is held to
 #endif
-#if GSR_BWD_WPE
 #define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_BWD_WPE, 8)))
-#else
-#define GSR_BWD_ATTR
-#endif
-#ifndef GSR_BWD_ANY
-#define GSR_BWD_ANY 1  // skip the wave reduction of pairs no pixel of the wave took (0: always reduce)
-#endif
-#ifndef GSR_BWD_QM_REG
-#define GSR_BWD_QM_REG 0  // 1: the quarter mask by v_readlane from the staging lane (measured 1.5 % slower)
-#endif
-#ifndef GSR_BWD_WAVES
-#define GSR_BWD_WAVES 4  // items (one wave each) per workgroup
-#endif
-constexpr int kBwdWaves = GSR_BWD_WAVES;
-#ifndef GSR_BWD_TRED
-#define GSR_BWD_TRED 0  // transposed pair reduction: pairs per LDS group (0: per-pair DPP reduction; 4-16 measured slower)
-#endif
-// Transposed reduction (GSR_BWD_TRED = G): a walked pair's 6 per-lane sums are folded over the wave's
-// lane halves and rows (3 permlane32 + 2 permlane16 swaps: 16 column sums of each value) and parked in
-// LDS; every G pairs the wave reads them back transposed -- 64 / G lanes per pair, each summing
-// 16 G / 64 columns with the column weights dx, dx^2, then a log2(64 / G)-stage DPP sum -- and
-// writes each pair's 9 sums into its s_out slot.  Replaces the per-pair weighting + 3 x 3 DPP row
-// stages + LDS atomics of wave_pair_sums with work spread over all lanes (fixed order: bitwise
-// reproducible).
-#if GSR_BWD_TRED
-constexpr int kTred = GSR_BWD_TRED;
-constexpr int kTredF = 96;  // floats per parked pair: 4 column-sum rows (64) + cs1 / cs2 columns (32)
-#endif
+constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
+
+// ---- the pair reduction ---------------------------------------------------------------------------
+// Every lane holds, for its 4 pixels of one column, S0 = sum sG, S1 = sum sG dy, S4 = sum sG dy^2 and
+// cs_c = sum w dL/dpix_c.  The rows of a column are folded first (3 permlane32 + 2 permlane16 swaps
+// on the 6 raw values), the column weights dx, dx^2 applied to the 16 column sums, and each 16-lane
+// row summed by 3 DPP stages into two halves (lanes of each parity: lanes 0 and 1 of the row hold
+// them, both added into the pair's LDS slot).  Row totals, slot = 4 * register + row:
+//   X rows: [sum dx S0, sum S4, sum S1, sum cs0]      (slots 0-3)
+//   Y rows: [sum dx^2 S0, sum cs1, sum dx S1, sum cs2] (slots 4-7)
+//   Z row 0: sum S0                                   (slot 8)
+// Fixed tree: bitwise reproducible.
+// The three row reductions of a pair, each 16-lane row summed by 3 DPP stages (row_ror 8, 4, 2) into
+// halves over the lanes of each parity -- lanes 0 and 1 of the row hold them.  Written out so that every
+// stage is one v_add_f32_dpp (the compiler keeps the last stage's move and add apart when the add sinks
+// into the storing lanes' branch); the three registers are interleaved, so each stage reads a register
+// written two instructions earlier (the VALU-write -> DPP-read hazard needs 2 wait states; the s_nop
+// covers the inputs' own writes).
+__device__ inline void row_halves3(float &X, float &Y, float &Z) {
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_add_f32_dpp %2, %2, %2 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(X), "+v"(Y), "+v"(Z));
+}
+struct RowW { float mx, cx, m0, m2; };  // per-lane weight coefficients of its row (see pair_sums)
+__device__ inline RowW row_weights(int row) {
+    return RowW{row == 0 ? 1.f : 0.f, row == 0 ? 0.f : 1.f, row == 0 ? 1.f : 0.f, row == 2 ? 1.f : 0.f};
+}
+struct PairSums { float X, Y, Z; };
+__device__ inline PairSums pair_sums(float S0, float S1, float S4, float cs0, float cs1, float cs2, float dx,
+                                     const RowW &w) {
+    const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(cs1, cs2);
+    const float rA = fold16(pA, pB);   // column sums, rows [S0, S4, S1, cs0]
+    const float rC = fold16(0.f, pC);  // rows [0, cs1, 0, cs2]
+    const float wx = fmaf(w.mx, dx, w.cx);       // row 0: dx, else 1
+    const float wy = dx * fmaf(w.m0, dx, w.m2);  // row 0: dx^2, row 2: dx, else 0
+    PairSums r{rA * wx, fmaf(rA, wy, rC), rA};
+    row_halves3(r.X, r.Y, r.Z);
+    return r;
+}
+
+// Per-pixel walk state of one quarter slot k.
+struct PixState { float T, AR, d0, d1, d2, fy; int lrel; };
+// Running per-lane sums of one walked pair.
+struct LaneSums { float S0, S1, S4, c0, c1, c2; };
+
+// One (pair, quarter) evaluation.  CLAMP: the pair's opacity can exceed 0.99, so alpha may be clamped
+// (wave-uniform, flagged at staging); otherwise alpha = o G exactly and sG = o G T (C - AR) = w (C - AR)
+// with w = alpha T, the colour weight -- the same product in fewer operations.  Branch-free: a pixel
+// that does not take the pair gets alpha = 0, which makes every update an identity (r = 1, AR
+// unchanged, zero sums).  The blend weight is pair_power + 2^x, the forward's exact operation
+// sequence, hence bitwise-identical decisions.
+template <bool CLAMP, bool EXACT>
+__device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &any, const PairX &x, float4 a,
+                                             float C2, float o, float4 c, int j, float pfx,
+                                             const float4 *__restrict__ rec, const uint32_t *__restrict__ pl) {
+    const float dy = a.y - ps.fy;  // same operation as the forward's
+    float p2 = pair_power(x, C2, dy);
+    float G = __builtin_amdgcn_exp2f(p2);
+    float alpha = CLAMP ? fminf(0.99f, o * G) : o * G;
+    const bool live = j < ps.lrel;  // the entry lies before this pixel's last contributor
+    if constexpr (EXACT) {  // the forward's near-threshold re-evaluation: the same decisions
+        const bool nr = live && near_threshold(alpha);
+        if (__builtin_amdgcn_ballot_w64(nr) && nr) {
+            const ExactBlend e = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * pl[j] + 3], o, pfx, ps.fy);
+            p2 = e.power; G = e.G; alpha = e.alpha;
+        }
+    }
+    const bool ok = live && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
+    any = any || ok;
+    const float al = ok ? alpha : 0.f;
+    ps.T = ps.T * __builtin_amdgcn_rcpf(1.f - al);  // T in front of the pair
+    const float cd = fmaf(c.z, ps.d2, fmaf(c.y, ps.d1, c.x * ps.d0));  // <colour, dL/dpix>
+    const float diff = cd - ps.AR;
+    ps.AR = fmaf(al, diff, ps.AR);
+    const float w = al * ps.T;
+    float gd;  // sG = o G T (C - AR), the reference's dL/dG * G scaled by the opacity
+    if constexpr (CLAMP) {
+        const float tg = ps.T * diff;
+        gd = ok ? (o * G) * tg : 0.f;  // the reference's alpha gradient ignores the 0.99 clamp
+    } else {
+        gd = w * diff;
+    }
+    const float u = gd * dy;
+    s.S0 += gd;
+    s.S1 += u;
+    s.S4 = fmaf(u, dy, s.S4);
+    s.c0 = fmaf(w, ps.d0, s.c0);
+    s.c1 = fmaf(w, ps.d1, s.c1);
+    s.c2 = fmaf(w, ps.d2, s.c2);
+}
+
+// The walk of one batch: every staged pair j (descending) over the quarters of its mask; each pair's
+// sums are reduced and added into its s_out slot when any pixel of the wave took it.  CLAMP: some
+// staged pair's opacity exceeds 0.99 (batch-uniform, so the pair loop itself has no variant branch).
+template <bool CLAMP, bool EXACT>
+__device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const float4 *s_a, float pfx,
+                                           const RowW &rw, float *o_row, const float4 *__restrict__ rec,
+                                           const uint32_t *__restrict__ pl) {
+    constexpr int kStage = 64 * kBwdWaves;
+    while (m) {
+        const int j = 63 - __builtin_clzll(m);
+        m &= ~(1ull << j);
+        const float4 a = s_a[j], b = s_a[kStage + j], c = s_a[2 * kStage + j];
+        // wave-uniform quarter mask of the staged entry
+        const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));
+        const PairX x = pair_x(a, pfx);
+        // -0 seeds: x + (-0) == x for every x, so the first contributor needs no add (the ISA folds it)
+        LaneSums s{-0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
+            eval_quarter<CLAMP, EXACT>(ps[k], s, any, x, a, b.x, b.y, c, j, pfx, rec, pl);
+        }
+        if (__builtin_amdgcn_ballot_w64(any)) {  // some pixel of the wave took the pair
+            const PairSums sm = pair_sums(s.S0, s.S1, s.S4, s.c0, s.c1, s.c2, x.dx, rw);
+            if ((threadIdx.x & 14) == 0) {  // lanes 0 and 1 of each row hold its two halves
+                float *o = o_row + j * kPartial;
+                lds_add(o, sm.X);
+                lds_add(o + 4, sm.Y);
+                if ((threadIdx.x & 63) < 2) lds_add(o + 8, sm.Z);
+            }
+        }
+    }
+}
+
 template <bool EXACT>
 __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
@@ -258,25 +365,19 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     // leaves the CUs' free slots to the forward kernels of the other streams in a pipelined step
     // (one-wave workgroups take every slot a finishing wave frees and starve their large-LDS
     // workgroups).
-    __shared__ float4 s_a_all[64 * kBwdWaves], s_b_all[64 * kBwdWaves], s_c_all[64 * kBwdWaves];
+    // Staging: one array, so the three record parts of entry j are at fixed offsets from one address
+    // (one address VGPR per pair, the rest immediate offsets).
+    constexpr int kStage = 64 * kBwdWaves;
+    __shared__ float4 s_stage[3 * kStage];
     __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
-#if GSR_BWD_TRED
-    __shared__ float s_park_all[kTred * kTredF * kBwdWaves];  // parked column sums (transposed reduction)
-    __shared__ uint32_t s_slot_all[kTred * kBwdWaves];        // staged index j of each parked pair
-#endif
     if (spec_ok && *spec_ok == 0u) return;  // speculative render half whose forward was redone: redone too
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t item = blockIdx.x * kBwdWaves + wv;
     if (item >= items[0].x) return;  // the launch covers the item bound
-    float4 *s_a = s_a_all + 64 * wv, *s_b = s_b_all + 64 * wv, *s_c = s_c_all + 64 * wv;
+    float4 *s_a = s_stage + 64 * wv;  // (x, y, A2, B2); + kStage: (C2, opacity, -, -); + 2 kStage: colour + mask
     float *s_out = s_out_all + 64 * kPartial * wv;
-#if GSR_BWD_TRED
-    float *s_park = s_park_all + kTred * kTredF * wv;
-    uint32_t *s_slot = s_slot_all + kTred * wv;
-#endif
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    uint32_t tr_evals = 0, tr_reds = 0;  // (pair, quarter) evaluations and wave reductions
 #endif
     const uint2 it = items[1 + item];
     const int tile = (int)it.x;
@@ -315,114 +416,37 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     // non-contributing pair (alpha = 0) leaves it untouched without a select.  The reference's
     // background term -T_final / (1 - alpha) <bg, dL/dpix> is carried inside AR: starting the
     // recurrence from the background seen through T_final gives exactly T_before (<c, dL/dpix> - AR).
-    float Tt[4], dp0[4], dp1[4], dp2[4], AR[4], pfy[4];
-    uint32_t lastc[4];
+    PixState ps[4];
     const uint32_t qmax[4] = {mq.x, mq.y, mq.z, mq.w};
     const bool has_bound = s1f < n;
     const size_t bidx = has_bound ? ((size_t)seg_off[tile] + seg) * kTilePix : 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int py = py0 + 4 * k;
-        pfy[k] = (float)py;
+        ps[k].fy = (float)py;
         const bool inside = px < W && py < H;
         const int pid = py * W + px;
         const float4 pe = inside ? pix_end[pid] : make_float4(0.f, 0.f, 0.f, 0.f);
-        lastc[k] = inside ? n_contrib[pid] : 0u;
-        dp0[k] = inside ? dL_dpixels[pid] : 0.f;
-        dp1[k] = inside ? dL_dpixels[H * W + pid] : 0.f;
-        dp2[k] = inside ? dL_dpixels[2 * H * W + pid] : 0.f;
+        // entry p lies before the pixel's last contributor iff p < n_contrib: kept relative to the
+        // batch start (lrel = n_contrib - start, advanced per batch)
+        ps[k].lrel = (inside ? (int)n_contrib[pid] : 0) - s1;
+        ps[k].d0 = inside ? dL_dpixels[pid] : 0.f;
+        ps[k].d1 = inside ? dL_dpixels[H * W + pid] : 0.f;
+        ps[k].d2 = inside ? dL_dpixels[2 * H * W + pid] : 0.f;
         float bd = 0;
-        bd += bg0 * dp0[k]; bd += bg1 * dp1[k]; bd += bg2 * dp2[k];
+        bd += bg0 * ps[k].d0; bd += bg1 * ps[k].d1; bd += bg2 * ps[k].d2;
         if (has_bound && qmax[k] >= (uint32_t)s1f) {  // wave-uniform: this quarter resumes at the boundary
             const float4 st = seg_state[bidx + 64 * k + lane];
-            Tt[k] = st.w;
-            const float behind = dp0[k] * (pe.x - st.x) + dp1[k] * (pe.y - st.y) + dp2[k] * (pe.z - st.z);
-            AR[k] = st.w > 0.f ? (behind + pe.w * bd) / st.w : bd;
+            ps[k].T = st.w;
+            const float behind = ps[k].d0 * (pe.x - st.x) + ps[k].d1 * (pe.y - st.y) + ps[k].d2 * (pe.z - st.z);
+            ps[k].AR = st.w > 0.f ? (behind + pe.w * bd) / st.w : bd;
         } else {
-            Tt[k] = pe.w;
-            AR[k] = bd;
+            ps[k].T = pe.w;
+            ps[k].AR = bd;
         }
     }
-    const int row = lane >> 4;
-    // s_out slots per pair: 0 sum dx S0, 1 sum S1, 2 sum dx^2 S0, 3 sum dx S1, 4 sum S4, 5 sum S0,
-    // 6..8 sum cs (the first five still to be scaled by the opacity); wave_pair_sums row map:
-#if !GSR_BWD_TRED
-    const int xslot = (row == 0) ? 0 : (row == 1) ? 4 : (row == 2) ? 1 : 6;
-    const int yslot = (row == 0) ? 2 : (row == 1) ? 7 : (row == 2) ? 3 : 8;
-#else
-    // transposed reduction: lane l reads parked pair l / kLps, columns (l % kLps) * kCpl ...
-    constexpr int kLps = 64 / kTred, kCpl = 16 / kLps;
-    static_assert(kTred >= 4 && kTred <= 16 && (kTred & (kTred - 1)) == 0, "GSR_BWD_TRED: 4, 8 or 16");
-    const int t_slot = lane / kLps, t_c0 = (lane % kLps) * kCpl;
-    int parked = 0;  // wave-uniform: pairs parked since the last flush
-    auto flush = [&](int n) {
-        wave_lds_sync();
-        if (t_slot < n) {
-            const uint32_t j = s_slot[t_slot];
-            const float gx = s_a[j].x;
-            const float *pk = s_park + t_slot * kTredF;
-            float *o = s_out + j * kPartial;
-            // three passes of three sums each (few live registers: the walk's per-pixel state is live)
-            auto reduce3 = [&](float a, float b, float c, int s0, int s1, int s2) {
-#pragma unroll
-                for (int d = 1; d < kLps; d <<= 1) {  // the slot's lanes are consecutive: xor butterfly
-                    a += __shfl_xor(a, d, 64);
-                    b += __shfl_xor(b, d, 64);
-                    c += __shfl_xor(c, d, 64);
-                }
-                if ((lane % kLps) == 0) { o[s0] = a; o[s1] = b; o[s2] = c; }
-            };
-            {   // row 0 (S0): sum, sum dx, sum dx^2
-                float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll
-                for (int k = 0; k < kCpl; ++k) {
-                    const float dx = gx - (tx0 + (float)(t_c0 + k));  // = pair_x's dx of the column
-                    const float v = pk[t_c0 + k], u = dx * v;
-                    a += v; b += u; c = fmaf(dx, u, c);
-                }
-                reduce3(a, b, c, 5, 0, 2);
-            }
-            {   // rows 1 (S4) and 2 (S1): sum S4, sum S1, sum dx S1
-                float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll
-                for (int k = 0; k < kCpl; ++k) {
-                    const float dx = gx - (tx0 + (float)(t_c0 + k));
-                    const float v = pk[32 + t_c0 + k];
-                    a += pk[16 + t_c0 + k]; b += v; c = fmaf(dx, v, c);
-                }
-                reduce3(a, b, c, 4, 1, 3);
-            }
-            {   // colour: row 3 (cs0) and the parked cs1 / cs2 columns
-                float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll
-                for (int k = 0; k < kCpl; ++k) {
-                    a += pk[48 + t_c0 + k]; b += pk[64 + t_c0 + k]; c += pk[80 + t_c0 + k];
-                }
-                reduce3(a, b, c, 6, 7, 8);
-            }
-        }
-        wave_lds_sync();
-    };
-#endif
-    // the batch ending at `e` (slots [max(e - 64, s0), e)): lane j's slot, its Gaussian's whole render
-    // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
-    // behind the current batch's pairs
-#if GSR_BWD_RECPF
-    // the batch ending at `e` (slots [max(e - 64, s0), e)): lane j's slot, its Gaussian's whole render
-    // record and its emission index, loaded one batch ahead of use so the gathers' latency hides
-    // behind the current batch's pairs
-    float4 a_n = make_float4(0.f, 0.f, 0.f, 0.f), b_n = a_n, c_n = a_n, cj_n = a_n;
-    uint32_t em_n = 0;
-    auto fetch = [&](int e) {
-        const int st = e - 64 > s0 ? e - 64 : s0;
-        if (lane < e - st) {
-            const uint32_t g = point_list[rg.x + st + lane];
-            em_n = slot_emit[rg.x + st + lane];
-            const float4 *r = rec + (size_t)kRecF4 * g;
-            a_n = r[0]; b_n = r[1]; c_n = r[2]; cj_n = r[3];
-        }
-    };
-#else
+    const RowW rw = row_weights(lane >> 4);
+    float *o_row = s_out + (lane >> 4);  // this lane's row slot of every pair's sums
     // the point list entry of each batch's slot is loaded one batch ahead (the render record gathers
     // depend on it); the records themselves are gathered at the batch start
     uint32_t g_n = 0, em_n = 0;
@@ -433,168 +457,61 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             em_n = slot_emit[rg.x + st + lane];
         }
     };
-#endif
     if (s1 > s0) fetch(s1);
     for (int end = s1; end > s0; end -= 64) {
         const int start = end - 64 > s0 ? end - 64 : s0;
         const int cnt = end - start;
         const uint32_t em = em_n;
-#if GSR_BWD_RECPF
-        const float4 a = a_n, b = b_n, c = c_n, cj = cj_n;
-#else
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, cj = a;
         if (lane < cnt) {
             const float4 *r = rec + (size_t)kRecF4 * g_n;
             a = r[0]; b = r[1]; c = r[2]; cj = r[3];  // cj: exact conic (a, b, c) of the staged Gaussian
         }
-#endif
         if (end - 64 > s0) fetch(end - 64);
 #pragma unroll
         for (int q = 0; q < kPartial; ++q) s_out[lane * kPartial + q] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ps[k].lrel += cnt;  // n_contrib - start
         // cull per 16x4 quarter: pixel slot k of every lane lies in rows 4k..4k+3 of the tile; a
         // quarter whose pixels all precede this slot in the forward's order (p >= its max
-        // n_contrib) is skipped too
+        // n_contrib) is skipped too.  Bit 4: the opacity can be clamped (alpha = min(0.99, o G)).
         uint32_t qmask = 0;
         if (lane < cnt) {
             const uint32_t p = (uint32_t)(start + lane);
-            s_a[lane] = a; s_b[lane] = b;
+            s_a[lane] = a;
+            s_a[kStage + lane] = b;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (p < qmax[k] &&
                     !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0 + 4 * k, tx1, ty0 + 4 * k + 3))
                     qmask |= 1u << k;
-            s_c[lane] = make_float4(c.x, c.y, c.z, __uint_as_float(qmask));  // .w: the quarter mask
+            if (qmask && b.y > 0.99f) qmask |= 16u;  // (the batch then takes the clamping walk)
+            s_a[2 * kStage + lane] = make_float4(c.x, c.y, c.z, __uint_as_float(qmask));  // .w: the quarter mask
         }
         uint64_t m = __ballot(qmask != 0);
         wave_lds_sync();
-#if GSR_BWD_PREFETCH
-        // the next pair's staged records are read from LDS while this pair is evaluated
-        int jn = m ? 63 - __builtin_clzll(m) : -1;
-        float4 an = make_float4(0.f, 0.f, 0.f, 0.f), bn = an, cn = an;
-        if (jn >= 0) { an = s_a[jn]; bn = s_b[jn]; cn = s_c[jn]; }
-        while (jn >= 0) {
-            const int j = jn;
-            m &= ~(1ull << j);
-            const float4 a = an, b = bn, c = cn;
-            jn = m ? 63 - __builtin_clzll(m) : -1;
-            if (jn >= 0) { an = s_a[jn]; bn = s_b[jn]; cn = s_c[jn]; }
-#else
-        while (m) {
-            const int j = 63 - __builtin_clzll(m);
-            m &= ~(1ull << j);
-            const float4 a = s_a[j], b = s_b[j], c = s_c[j];
-#endif
-            const uint32_t p = (uint32_t)(start + j);
-            // wave-uniform quarter mask, read from the staging lane's register (not the LDS copy), so
-            // the scalar branches below need not wait for the LDS reads
-            const uint32_t qm = GSR_BWD_QM_REG ? __builtin_amdgcn_readlane(qmask, j)
-                                               : __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));
-            const PairX x = pair_x(a, pfx);
-            // per-lane sums over this lane's pixels: S0 = sum G dL/dalpha, S1 = sum G dL/dalpha dy,
-            // S4 = sum G dL/dalpha dy^2, cs = sum alpha T dL/dpix (the lane's 4 pixels share dx)
-            // -0 seeds: x + (-0) == x for every x, so the first contributor needs no add (the ISA folds it)
-            float S0 = -0.f, S1 = -0.f, S4 = -0.f, cs0 = -0.f, cs1 = -0.f, cs2 = -0.f;
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
-                // branch-free: a non-contributing pixel gets alpha = 0, which makes every update an
-                // identity (r = 1, AR unchanged, zero sums)
-                const float dy = a.y - pfy[k];  // same operation as the forward's (bitwise-equal decisions)
-                float p2 = pair_power(x, b.x, dy);
-                float G = __builtin_amdgcn_exp2f(p2);
-                float alpha = fminf(0.99f, b.y * G);
-                if constexpr (EXACT) {  // the forward's near-threshold re-evaluation: the same decisions
-                    const bool nr = p < lastc[k] && near_threshold(alpha);
-                    if (__ballot(nr) && nr) {
-                        const uint32_t g = point_list[rg.x + p];
-                        const ExactBlend e = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy[k]);
-                        p2 = e.power; G = e.G; alpha = e.alpha;
-                    }
-                }
-                const bool ok = p < lastc[k] && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
-                any = any || ok;
-                const float al = ok ? alpha : 0.f;
-                const float r = __builtin_amdgcn_rcpf(1.f - al);
-                Tt[k] = Tt[k] * r;
-                const float cd = fmaf(c.z, dp2[k], fmaf(c.y, dp1[k], c.x * dp0[k]));  // <colour, dL/dpix>
-                const float diff = cd - AR[k];
-                const float dLa = diff * Tt[k];
-                AR[k] = fmaf(al, diff, AR[k]);
-                const float gd = ok ? G * dLa : 0.f;
-                const float u = gd * dy;
-                S0 += gd;
-                S1 += u;
-                S4 = fmaf(u, dy, S4);
-                const float dch = al * Tt[k];
-                cs0 = fmaf(dch, dp0[k], cs0);
-                cs1 = fmaf(dch, dp1[k], cs1);
-                cs2 = fmaf(dch, dp2[k], cs2);
-            }
-#ifdef GSR_TRACE
-            tr_evals += __builtin_popcount(qm);
-            tr_reds += __ballot(any) ? 1u : 0u;
-#endif
-#if GSR_BWD_TRED
-            if (!GSR_BWD_ANY || __ballot(any)) {
-                // fold the 6 sums to 16 column sums each and park them; reduced every kTred pairs
-                const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(cs1, cs2);
-                const float rA = fold16(pA, pB);  // rows [S0, S4, S1, cs0]
-                const float rC = fold16(pC, pC);  // rows [cs1, cs1, cs2, cs2]
-                float *pk = s_park + parked * kTredF;
-                pk[lane] = rA;
-                if (!(row & 1)) pk[64 + (row >> 1) * 16 + (lane & 15)] = rC;
-                if (lane == 0) s_slot[parked] = (uint32_t)j;
-                if (++parked == kTred) {
-                    flush(kTred);
-                    parked = 0;
-                }
-            }
-#else
-            if (!GSR_BWD_ANY || __ballot(any)) {
-                // moments of G dL/dalpha over the tile: (dx, dy, dx^2, dx dy, dy^2) (opacity later)
-                const PairSums sm = wave_pair_sums(S0, S1, S4, cs0, cs1, cs2, x.dx, row);
-                if ((lane & 15) < kRedLanes) {  // the first kRedLanes lanes of each row hold its partial
-                    // sums, added into the zeroed slot (2 lanes: 0 + h0 + h1 == h0 + h1 in either order)
-                    float *o = s_out + j * kPartial;
-#if GSR_BWD_RED_STAGES >= 4
-                    o[xslot] = sm.X;  // one lane per row: every slot is written once per pair
-                    o[yslot] = sm.Y;
-                    if (lane == 0) o[5] = sm.Z;
-#else
-                    lds_add(o + xslot, sm.X);
-                    lds_add(o + yslot, sm.Y);
-                    if (lane < kRedLanes) lds_add(o + 5, sm.Z);
-#endif
-                }
-            }
-#endif
-        }
-#if GSR_BWD_TRED
-        if (parked) {
-            flush(parked);
-            parked = 0;
-        }
-#endif
+        const uint32_t *pl = point_list + rg.x + start;
+        if (__builtin_amdgcn_ballot_w64(qmask & 16u)) walk_batch<true, EXACT>(ps, m, s_a, pfx, rw, o_row, rec, pl);
+        else walk_batch<false, EXACT>(ps, m, s_a, pfx, rw, o_row, rec, pl);
         wave_lds_sync();
         if (lane < cnt) {
             const float *s2 = s_out + lane * kPartial;
             float sm[kPartial];
 #pragma unroll
             for (int q = 0; q < kPartial; ++q) sm[q] = s2[q];
-            const float o = s_b[lane].y;  // the moments of sG = opacity G dL/dalpha
-            const float S1 = o * sm[0], S2 = o * sm[1];
+            // sums of sG = o G dL/dalpha: the opacity is already in; dL/dopacity = sum G dL/dalpha
             rec_store(part, em,
-                      (-cj.x * S1 - cj.y * S2) * half_w,   // dL/dmeans2D.x (NDC)
-                      (-cj.y * S1 - cj.z * S2) * half_h,   // dL/dmeans2D.y (NDC)
-                      -0.5f * (o * sm[2]),                 // dL/dconic.a
-                      -0.5f * (o * sm[3]),                 // dL/dconic.b (b/2 convention)
-                      -0.5f * (o * sm[4]),                 // dL/dconic.c
-                      sm[5], sm[6], sm[7], sm[8]);         // dL/dopacity, dL/dcolour
+                      (-cj.x * sm[0] - cj.y * sm[2]) * half_w,  // dL/dmeans2D.x (NDC)
+                      (-cj.y * sm[0] - cj.z * sm[2]) * half_h,  // dL/dmeans2D.y (NDC)
+                      -0.5f * sm[4],                            // dL/dconic.a
+                      -0.5f * sm[6],                            // dL/dconic.b (b/2 convention)
+                      -0.5f * sm[1],                            // dL/dconic.c
+                      sm[8] != 0.f ? sm[8] / b.y : 0.f,         // dL/dopacity
+                      sm[3], sm[5], sm[7]);                     // dL/dcolour
         }
     }
 #ifdef GSR_TRACE
-    trace_wave(g_trace_bwd, item, t_start, tr_evals | ((uint64_t)tr_reds << 32));
+    trace_wave(g_trace_bwd, item, t_start, 0);
 #endif
 }
 

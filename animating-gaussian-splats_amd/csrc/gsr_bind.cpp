@@ -412,6 +412,9 @@ void backward_views(const py::list &views, const at::Tensor &means3D, const at::
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "native argument marshalling for diff_gaussian_rasterization._C (libgsr's C ABI)";
     m.def("set_functions", &set_functions);
+    // the include/gsr.h ABI this build's structs follow: _C.py falls back to ctypes when it differs
+    // from the loaded library's gsr_abi_version() (a stale build would pass wrongly sized structs)
+    m.def("abi_version", []() { return (int)GSR_ABI_VERSION; });
     m.def("forward", &forward);
     m.def("backward_render", &backward_render);
     m.def("backward_views", &backward_views);

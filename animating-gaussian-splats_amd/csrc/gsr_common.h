@@ -643,6 +643,12 @@ __device__ inline void lds_barrier() {
     __syncthreads();
 }
 
+// Wait until every vector-memory operation of this wave -- its device-scope atomics included -- has
+// completed (gfx9 encoding: vmcnt(0), expcnt / lgkmcnt at maximum).  A workgroup-scope release fence
+// does not wait for them (it compiles to an LDS wait only), so a block that counts itself done with
+// an atomic after its other atomics puts this, then its barrier, in front of the done counter.
+__device__ inline void drain_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // Make this wave's LDS writes visible to its own later LDS reads (waves of a render block work
 // on different tiles and never synchronise with each other).
 __device__ inline void wave_lds_sync() {
@@ -786,13 +792,7 @@ __device__ inline bool tile_cull(float gx, float gy, float a, float b, float c, 
     return qmin > tau * 1.001f + 1e-3f;
 }
 
-// ---- cross-lane sum of 9 values over a wave64 (gfx950) -------------------------------------
-// Folds pairs of values across lane halves with v_permlane32_swap, across rows with
-// v_permlane16_swap, then reduces each 16-lane row with DPP.  Totals end up in:
-//   r0123: lane 0 -> v0, lane 16 -> v2, lane 32 -> v1, lane 48 -> v3
-//   r4567: lane 0 -> v4, lane 16 -> v6, lane 32 -> v5, lane 48 -> v7
-//   r8   : lane 0 -> v8
-// (every lane of a row holds its row's total).  Fixed tree: bitwise reproducible.
+// ---- cross-lane folds over a wave64 (gfx950) ----------------------------------------------
 // No-return LDS float add (ds_add_f32).
 __device__ inline void lds_add(float *p, float v) {
     (void)__hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -806,76 +806,4 @@ __device__ inline float fold16(float a, float b) {  // rows (a0+a1, b0+b1, a2+a3
     auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-__device__ inline float row_sum16(float v) {  // every lane of each 16-lane row gets the row sum
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-    return v;
-}
-// Three of the four row_sum16 stages: lane l of a row ends with the sum over the row's lanes of l's
-// parity, so lanes 0 and 1 of each row hold the two halves of the row total (the last DPP stage, a
-// quad_perm that compiles to a DPP move + add, is left to the consumer's single add).
-__device__ inline float row_sum16_pairs(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
-    // quad_perm 2,3,0,1 reads a valid lane everywhere: bound_ctrl, so the DPP move needs no zeroed
-    // destination first (one v_mov fewer per call)
-    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
-    return v;
-}
-
-// Per-pair gradient sums of the backward blend (k_render_bwd): each lane holds, for its 4 pixels of
-// one column, S0 = sum sG, S1 = sum sG dy, S4 = sum sG dy^2 and cs_c = sum alpha T dL/dpix_c.  The 9
-// wave sums the record needs are sum S0, sum dx S0, sum dx^2 S0, sum S1, sum dx S1, sum S4, sum cs_c
-// with dx = the column's offset, so the rows of a column are folded FIRST (3 + 2 permlane swaps on
-// the 6 raw values instead of 5 + 3 on 9 weighted ones), the column weights dx, dx^2 applied to the
-// column sums, and each 16-lane row summed with DPP to two halves (row_sum16_pairs: lanes 0 and 1 of
-// a row hold them).  Row totals:
-//   X rows: [sum dx S0, sum S4, sum S1, sum cs0]    Y rows: [sum dx^2 S0, sum cs1, sum dx S1, sum cs2]
-//   Z row 0: sum S0
-// GSR_BWD_RED_STAGES: DPP stages of the row sums (4: lane 0 of a row holds its total, stored plainly;
-// 3: lanes 0-1 of a row hold its halves; 2: lanes
-// 0-3 its quarters; 1: lanes 0-7 its eighths) -- the rest is added by LDS atomics into the slot
-#ifndef GSR_BWD_RED_STAGES
-#define GSR_BWD_RED_STAGES 3
-#endif
-constexpr int kRedLanes = 16 >> GSR_BWD_RED_STAGES;  // lanes per row that add their partial sum
-__device__ inline float row_sum16_part(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false)); // row_ror:8
-    if (GSR_BWD_RED_STAGES >= 2)
-        v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false)); // row_ror:4
-    if (GSR_BWD_RED_STAGES >= 3)
-        v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
-    if (GSR_BWD_RED_STAGES >= 4)  // lane 0 of the row holds the whole row sum: a plain LDS store, no atomics
-        v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
-    return v;
-}
-struct PairSums { float X, Y, Z; };
-__device__ inline PairSums wave_pair_sums(float S0, float S1, float S4, float cs0, float cs1, float cs2,
-                                          float dx, int row) {
-    const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(cs1, cs2);
-    const float rA = fold16(pA, pB);   // column sums, rows [S0, S4, S1, cs0]
-    const float rC = fold16(0.f, pC);  // rows [0, cs1, 0, cs2]
-    const float wx = row == 0 ? dx : 1.f;
-    const float wy = row == 0 ? dx * dx : (row == 2 ? dx : 0.f);
-    PairSums r;
-    r.X = row_sum16_part(rA * wx);
-    r.Y = row_sum16_part(fmaf(rA, wy, rC));
-    r.Z = row_sum16_part(rA);
-    return r;
-}
-
-struct Sum9 { float r0123, r4567, r8; };
-__device__ inline Sum9 wave_sum9(float v0, float v1, float v2, float v3, float v4, float v5, float v6,
-                                 float v7, float v8) {
-    const float p01 = fold32(v0, v1), p23 = fold32(v2, v3), p45 = fold32(v4, v5), p67 = fold32(v6, v7);
-    const float p8 = fold32(v8, 0.f);
-    Sum9 s;
-    s.r0123 = row_sum16(fold16(p01, p23));
-    s.r4567 = row_sum16(fold16(p45, p67));
-    s.r8 = row_sum16(fold16(p8, 0.f));
-    return s;
-}
-
 }  // namespace gsr

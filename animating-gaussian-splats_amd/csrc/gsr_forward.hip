@@ -194,28 +194,11 @@ __global__ __launch_bounds__(kBinThreads) void k_bin_count(int P, int CH, int T,
 // (done counter) turns the LPT bucket counts into offsets (k_bin_emit scatters the dispatch order),
 // scans the chunk sums into chunk emission offsets and publishes K and the list classes to meta and
 // the host words -- as k_bin_scan does.
-#ifndef GSR_COLSCAN_W
-#define GSR_COLSCAN_W 32  // tile columns per k_bin_colscan block (32 x kColG threads)
-#endif
-constexpr int kColW = GSR_COLSCAN_W, kColG = 32, kColR = 16;
+constexpr int kColW = 32, kColG = 32, kColR = 16;  // tile columns x chunk groups per k_bin_colscan block
 static_assert(kColG * kColR >= 512, "BinGrid makes at most 512 chunks");
 static_assert(kColW <= 64 && kMaxLdsTiles <= kColW * kScanBlocksMax, "look-back: one wave per block, <= kScanBlocksMax blocks");
-// Slab order inside a tile's range (GSR_XCD_SLABS=1, not the default): the chunks k_bin_emit would run
-// on one XCD under round-robin dispatch (chunk b on XCD b % 8) adjacent, so that XCD's scattered pair
-// stores into a tile form one run.  Measured against chunk order: k_bin_emit alone 47 vs 54 us, but its
-// written bytes 130 vs 102 MB per launch and, inside the 3-stream step, bin_emit 214-218 -> 327-341 us
-// and tile_sort 41 -> 99-148 us; the step 1354-1366 vs 1357-1381 Msplats/s (tools/r04_xcd_ab.sh).
-#ifndef GSR_XCD_SLABS
-#define GSR_XCD_SLABS 0
-#endif
-__device__ inline int slab_chunk(int k, int NB) {  // the chunk at slab position k of a tile's range
-    if (!GSR_XCD_SLABS) return k;
-    const int q = NB >> 3, r = NB & 7, big = r * (q + 1);
-    int x, i;
-    if (k < big) { x = k / (q + 1); i = k - x * (q + 1); }
-    else { const int k2 = k - big; x = r + k2 / q; i = k2 - (x - r) * q; }
-    return i * 8 + x;
-}
+// Slabs inside a tile's range follow chunk order (an XCD-grouped order was faster alone but slower in
+// the 3-stream step).
 __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
     int T, int NB, uint32_t *__restrict__ chunk_off, uint32_t *__restrict__ tile_count, uint2 *__restrict__ ranges,
     uint32_t *__restrict__ tile_cursor, uint32_t *__restrict__ seg_off, uint32_t *__restrict__ sort_lists,
@@ -228,11 +211,9 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
     __shared__ uint32_t s_lpt[kOrderBuckets];  // this block's tiles per LPT bucket, then the block's base
     uint64_t *look = reinterpret_cast<uint64_t *>(ws);
     uint32_t *ctr = ws + 2 * kScanBlocksMax, *lpt = ctr + kScanCtr;
-#ifndef GSR_SCAN_TICKET
-#define GSR_SCAN_TICKET 0  // 1: blocks take their columns by an atomic ticket (0: blockIdx -- a grid is
-                           // dispatched in block order, so every block a look-back waits on is resident)
-#endif
-    if (threadIdx.x == 0) s_blk = GSR_SCAN_TICKET ? atomicAdd(&ctr[0], 1u) : blockIdx.x;
+    // blocks take their columns by blockIdx: a grid is dispatched in block order, so every block a
+    // look-back waits on is resident
+    if (threadIdx.x == 0) s_blk = blockIdx.x;
     for (int i = threadIdx.x; i < kOrderBuckets; i += blockDim.x) s_lpt[i] = 0;
     __syncthreads();
     const int blk = (int)s_blk;
@@ -245,7 +226,7 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < kColR; ++k) {  // slab positions r0 .. r1 - 1 of this group
-        v[k] = (t < T && r0 + k < r1) ? p[(size_t)slab_chunk(r0 + k, NB) * T] : 0u;
+        v[k] = (t < T && r0 + k < r1) ? p[(size_t)(r0 + k) * T] : 0u;
         sum += v[k];
     }
     s_part[grp][col] = sum;
@@ -261,7 +242,7 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
         if (grp == 0) tile_count[t] = tot;
 #pragma unroll
         for (int k = 0; k < kColR; ++k) {
-            if (r0 + k < r1) p[(size_t)slab_chunk(r0 + k, NB) * T] = pre;
+            if (r0 + k < r1) p[(size_t)(r0 + k) * T] = pre;
             pre += v[k];
         }
     }
@@ -325,8 +306,9 @@ __global__ __launch_bounds__(kColW * kColG) void k_bin_colscan(
     // No agent-scope fences: the 8 XCDs' L2s are not coherent, so such a fence writes back / invalidates
     // the whole L2 (a first version with __threadfence() and acquire / release look-back words took
     // ~100 us).  Everything another block reads here is a device-scope atomic (payload and flag share
-    // one word); the wave drains its own atomics (workgroup-scope fence: a vmcnt wait) before the block
-    // counts itself done.
+    // one word); every wave drains its own atomics (an explicit vmcnt(0): the workgroup-scope fence
+    // waits for LDS only) before the block counts itself done.
+    drain_vmem();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) s_last = atomicAdd(&ctr[1], 1u) == gridDim.x - 1 ? 1u : 0u;
@@ -898,11 +880,6 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const int n = (int)(rg.y - rg.x);
     const bool sorted_here = n <= kFwdSortCap;
     if (n > 0 && sorted_here) {
-#ifdef GSR_FWD_NOSORT  // timing experiment only (wrong order): the share of the in-render sort
-        for (int i = threadIdx.x; i < n; i += 256) { const uint4 q = pairs[rg.x + i]; s_key[i] = pair_key(q); s_u.val[i] = q.z; }
-        __syncthreads();
-        if (false)
-#endif
         if (n <= 256) block_sort_tile<1, 4>(n, rg.x, pairs, s_key, s_u.val);
         else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, pairs, s_key, s_u.val);
         else block_sort_tile<4, 4>(n, rg.x, pairs, s_key, s_u.val);

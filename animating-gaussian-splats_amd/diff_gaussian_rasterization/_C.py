@@ -341,14 +341,19 @@ def _native():
             import importlib.machinery
             import importlib.util
             L = load_library()
-            spec = importlib.util.spec_from_file_location(
-                "gsr_bind", path, loader=importlib.machinery.ExtensionFileLoader("gsr_bind", path))
-            m = importlib.util.module_from_spec(spec)
-            try:
+            import warnings
+            try:  # the dlopen + PyInit happen in module_from_spec, the module body in exec_module
+                spec = importlib.util.spec_from_file_location(
+                    "gsr_bind", path, loader=importlib.machinery.ExtensionFileLoader("gsr_bind", path))
+                m = importlib.util.module_from_spec(spec)
                 spec.loader.exec_module(m)
-            except ImportError as err:  # a stale build (another torch): the ctypes marshalling, same kernels
-                import warnings
+                abi = m.abi_version() if hasattr(m, "abi_version") else None
+            except (ImportError, OSError) as err:  # a stale build (another torch): ctypes, same kernels
                 warnings.warn(f"gsr_bind.so not loadable ({err}); binding libgsr through ctypes instead")
+                return None
+            if abi != L.gsr_abi_version():  # built against another include/gsr.h: its structs differ
+                warnings.warn(f"gsr_bind.so built for ABI {abi}, libgsr.so is ABI {L.gsr_abi_version()}: "
+                              "binding libgsr through ctypes instead (rebuild gsr_bind)")
                 return None
             m.set_functions({n: ctypes.cast(L[n], ctypes.c_void_p).value for n in (  # (L[n]: the symbol itself)
                 "gsr_forward_info_call", "gsr_forward_async", "gsr_backward_render", "gsr_backward_gaussians",
@@ -547,12 +552,7 @@ def _forward(background, means3D, colors, opacity, scales, rotations, scale_modi
             L, background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
             projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, activations,
             prepare_backward, speculate, nonblocking)
-    dev = means3D.device
     pending = AsyncForward(fi.pending) if fi.pending else None
-    if fi.aux_stream:  # the item list is written into BINNING on the library's auxiliary stream: no early reuse
-        bb = alloc.base_of(GSR_BUF_BINNING)
-        if bb is not None:
-            bb.record_stream(_external_stream(fi.aux_stream, dev))
     return fi, color, radii, depth, alloc, pending
 
 

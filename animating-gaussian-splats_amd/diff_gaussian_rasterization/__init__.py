@@ -412,169 +412,7 @@ def _try_defer(ctx, gauss, radii, geomBuffer, leaf_inputs, nodes, need, render_f
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
     args = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
-    if _view_stream_call(args):
-        return _on_view_stream(args, raster_settings)
     return _RasterizeGaussians.apply(*args, raster_settings, torch.is_grad_enabled())
-
-
-# ---- library view streams for non-leaf inputs (the unchanged train.py / densify.py call shape) ------
-# train.py renders its 5 views from one thread on torch's current stream C with NON-leaf inputs
-# (create_render_arguments: normalize / sigmoid / exp / zeros + 0, shared.py:29-42) and one backward of
-# the summed losses (train.py:402-418).  Every gradient the rasterizer returns then goes to a node of the
-# caller's graph that ran on C, and the autograd engine makes C wait for the producing stream the moment
-# it hands a gradient over (InputBuffer::add), i.e. right after the producing node returns.  The engine
-# runs ready nodes by descending sequence number, so the rasterizer node of view k (created after view
-# k-1's loss) runs before view k-1's loss backward and C waits for it before that loss backward: the
-# views' backward kernels would run strictly one after another, whatever stream they were queued on.
-# Here each such view runs on one of the library's view streams L (round robin): L waits for C, the
-# forward is queued on L, C waits for L before the outputs are used (the forward stays ordered as the
-# caller wrote it).  The rasterizer node itself is created by a helper thread: sequence numbers are per
-# thread, so it has the lowest priority of the pass -- the engine runs every view's loss backward first,
-# then the rasterizer nodes, each queuing its view's backward on that view's L right away (they overlap
-# on the GPU), and the caller's consumers on C wait for each L as the engine hands the gradients over.
-# Gradients made on L and read on C are record_stream'ed on C; leaf gradients are added into .grad in
-# place on L, and the end of the pass makes C wait for every L it used.  Results are bitwise those of
-# one stream: every gradient write is ordered (ordered_grad_write) and each consumer waits for its
-# producer.  Off by default (GSR_VIEW_STREAMS=1 / set_view_streams(True) turn it on): measured on the
-# unchanged train.py step the views' kernels overlap but the step does not get shorter -- the render
-# kernels are VALU-bound and slow each other down when they share the chip, and the hand-off adds host
-# time -- 1014-1031 Msplats/s without, 955-970 with.
-_VIEW_STREAMS = {"on": os.environ.get("GSR_VIEW_STREAMS", "0") == "1", "n": int(os.environ.get("GSR_VIEW_STREAMS_N", "3")),
-                 "pool": {}, "next": {}, "helper": os.environ.get("GSR_VIEW_HELPER", "1") != "0"}
-
-
-def set_view_streams(on: bool) -> bool:
-    """Enable / disable the library view streams for non-leaf inputs; returns the previous setting."""
-    prev = _VIEW_STREAMS["on"]
-    _VIEW_STREAMS["on"] = bool(on)
-    return prev
-
-
-def _view_stream_call(args):
-    """Does this call take a view stream: enabled, grad mode, GPU inputs, and an input that is not a leaf
-    but requires grad (its gradient goes to a node of the caller's graph)."""
-    if not _VIEW_STREAMS["on"] or not torch.is_grad_enabled() or not args[0].is_cuda:
-        return False
-    return any(isinstance(t, torch.Tensor) and t.requires_grad and not t.is_leaf and t.numel() for t in args)
-
-
-def _view_stream(dev):
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
-    pool = _VIEW_STREAMS["pool"].get(key)
-    if pool is None:
-        pool = _VIEW_STREAMS["pool"][key] = [torch.cuda.Stream(torch.device("cuda", key))
-                                              for _ in range(_VIEW_STREAMS["n"])]
-    k = _VIEW_STREAMS["next"].get(key, 0)
-    _VIEW_STREAMS["next"][key] = (k + 1) % len(pool)
-    return pool[k]
-
-
-class _HelperThread:
-    """The thread that creates the view-stream rasterizer nodes (its autograd sequence numbers stay far
-    below the caller's, which makes dozens of nodes per view); one synchronous hand-off per render."""
-
-    def __init__(self):
-        import queue
-        self.q = queue.SimpleQueue()
-        self.t = threading.Thread(target=self._run, name="gsr-views", daemon=True)
-        self.t.start()
-
-    def _run(self):
-        while True:
-            job, done, box = self.q.get()
-            try:
-                box["out"] = job()
-            except BaseException as e:  # noqa: BLE001 - re-raised in the caller
-                box["err"] = e
-            done.release()
-
-    def call(self, job):
-        done, box = threading.Lock(), {}
-        done.acquire()
-        self.q.put((job, done, box))
-        done.acquire()  # released by the helper when the job is done
-        if "err" in box:
-            raise box["err"]
-        return box["out"]
-
-
-_helper = None
-_helper_lock = threading.Lock()
-_sync_tasks = {}  # graph task -> the (caller stream, view streams) its end-of-pass callback joins
-
-
-_STREAMS = {}  # raw HIP stream -> torch Stream object (torch.cuda.current_stream builds a new one per call)
-_EVENTS = {}   # (caller stream, view stream) -> (fork event, join event), re-recorded every call
-
-
-def _current_stream(idx):
-    raw = _C._raw_stream(idx)
-    st = _STREAMS.get(raw)
-    if st is None:
-        st = _STREAMS[raw] = torch.cuda.current_stream(idx)
-    return st
-
-
-def _on_view_stream(args, rs):
-    global _helper
-    dev = args[0].device
-    idx = dev.index if dev.index is not None else _C._get_device()
-    C = _current_stream(idx)
-    L = _view_stream(dev)
-    evs = _EVENTS.get((C.cuda_stream, L.cuda_stream))
-    if evs is None:
-        evs = _EVENTS[(C.cuda_stream, L.cuda_stream)] = (torch.cuda.Event(), torch.cuda.Event())
-    evs[0].record(C)
-    L.wait_event(evs[0])  # the caller's inputs (activations) are ready on L
-    for t in args:
-        if t.numel() and t.is_cuda:
-            t.record_stream(L)  # read on L (forward and backward): no early reuse on C
-    if _helper is None and _VIEW_STREAMS["helper"]:
-        with _helper_lock:
-            if _helper is None:
-                _helper = _HelperThread()
-
-    def job():
-        with torch.enable_grad(), torch.cuda.device(dev), torch.cuda.stream(L):
-            _view_tls.cur = (C, L)  # read by the Function's forward (this thread, synchronous)
-            try:
-                return _RasterizeGaussians.apply(*args, rs, True)
-            finally:
-                _view_tls.cur = None
-    # without the helper the node gets the caller's sequence numbers: with ONE view stream the engine
-    # then runs view k's consumers (on C) before view k-1's rasterizer backward (on L), which still
-    # overlaps them
-    color, radii, depth = _helper.call(job) if _VIEW_STREAMS["helper"] else job()
-    for t in (color, radii, depth):
-        t.record_stream(C)
-    evs[1].record(L)
-    C.wait_event(evs[1])  # the outputs are used on the caller's stream
-    return color, radii, depth
-
-
-_view_tls = threading.local()
-
-
-def _view_stream_backward(ctx):
-    """Called from the rasterizer's backward node when its forward ran on a view stream: the backward
-    pass gets one end-of-pass callback that makes the caller's stream wait for every view stream the
-    pass used (leaf gradients are written in place there)."""
-    task = torch._C._current_graph_task_id()
-    if task < 0:
-        return
-    with _helper_lock:
-        ent = _sync_tasks.get(task)
-        new = ent is None
-        if new:
-            ent = _sync_tasks[task] = (ctx.view_caller, set())
-        ent[1].add(ctx.view_stream)
-    if new:
-        def join():
-            with _helper_lock:
-                caller, streams = _sync_tasks.pop(task, (None, ()))
-            for st in streams:
-                caller.wait_stream(st)
-        torch.autograd.Variable._execution_engine.queue_callback(join)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
@@ -595,7 +433,6 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.binning_layout = fi.binning_layout
         ctx.pending = pending  # an asynchronous forward: resolved by the backward
         ctx.bufs = _buffer_ptrs(alloc)  # GEOM, BINNING, IMAGE device pointers (the bases are saved)
-        ctx.view_caller, ctx.view_stream = getattr(_view_tls, "cur", None) or (None, None)
         # leaves whose existing gradient the backward kernel may accumulate into (grad output order)
         ctx.leaves = (means2D, colors_precomp, opacities, means3D, cov3Ds_precomp, sh, scales, rotations)
         ctx.tensor_pos = _tensor_positions((means3D, means2D, sh, colors_precomp, opacities, scales,
@@ -608,8 +445,6 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, grad_depth):
-        if ctx.view_stream is not None:
-            _view_stream_backward(ctx)
         if grad_out_color is None:  # only depth was used: it carries no gradient (-w-depth)
             return (None,) * 10
         rs = ctx.raster_settings
@@ -642,10 +477,6 @@ class _RasterizeGaussians(torch.autograd.Function):
         for k, t in enumerate(acc):
             if t is not None:
                 g[k] = None  # already accumulated into the leaf's .grad
-        if ctx.view_stream is not None:  # made on the view stream, read by the caller's graph on C
-            for t in g:
-                if t is not None:
-                    t.record_stream(ctx.view_caller)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp,
          grad_sh, grad_scales, grad_rotations) = g
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities,

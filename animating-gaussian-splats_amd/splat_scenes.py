@@ -144,6 +144,30 @@ def scene_cameras(cfg: SceneConfig, device="cuda"):
                             sh_degree=sh) for yaw, h in cfg.views]
 
 
+# The inference renders of train.py (render_and_export_frame, train.py:506-547, under torch.no_grad() at
+# train.py:778): five fixed cameras (create_extrinsic_matrices, train.py:459-503) at 1280 x 720 with the
+# intrinsic [[a W, 0, W / 2], [0, a W, H / 2], [0, 0, 1]] of each camera's aspect ratio a (train.py:512-525).
+INFERENCE_W, INFERENCE_H = 1280, 720
+
+
+def inference_rig() -> dict:
+    """name -> (w2c, aspect ratio), restating create_extrinsic_matrices (train.py:459-503)."""
+    d, h = 2.4, 1.3
+    top = np.array([[1.0, 0.0, 0.0, 0.0], [0.0, 0.0, -1.0, 0.0], [0.0, 1.0, 0.0, 4.5], [0.0, 0.0, 0.0, 1.0]])
+    return {"000": (look_at(0, h, d), 0.82), "090": (look_at(90, h, d), 0.52), "180": (look_at(180, h, d), 0.52),
+            "270": (look_at(270, h, d), 0.52), "top": (top, 0.35)}
+
+
+def inference_intrinsics(aspect: float, width: int = INFERENCE_W, height: int = INFERENCE_H) -> np.ndarray:
+    return np.array([[aspect * width, 0, width / 2], [0, aspect * width, height / 2], [0, 0, 1]])
+
+
+def inference_cameras(device="cuda"):
+    """The five GaussianRasterizationSettings render_and_export_frame builds (sh_degree 0, zero bg)."""
+    return [render_settings(INFERENCE_W, INFERENCE_H, inference_intrinsics(a), w2c, device=device)
+            for w2c, a in inference_rig().values()]
+
+
 def activated_inputs(params: dict, sh_degree: int = -1) -> dict:
     """Rasterizer inputs (``create_render_arguments`` plus SH when configured) as plain tensors."""
     a = render_arguments(params)

@@ -92,8 +92,9 @@ class RenderStep:
                 imgs = [None] * len(views)
                 for k, f in enumerate(futs):
                     imgs[k::ns] = f.result()
-            else:  # one submitting thread: the device once, the stream switched per view and restored
+            else:  # one submitting thread: the device once, the stream switched per view; both restored
                 imgs = []
+                prev_dev = torch.cuda.current_device()
                 torch.cuda.set_device(self.device)
                 cur = torch.cuda.current_stream(self.device)
                 try:
@@ -102,6 +103,7 @@ class RenderStep:
                         imgs.append(GaussianRasterizer(raster_settings=self.cams[ci])(**self.inputs_of(ci))[0])
                 finally:
                     torch.cuda.set_stream(cur)
+                    torch.cuda.set_device(prev_dev)
             torch.autograd.backward(imgs, [self.dl] * len(imgs))
             return [img.detach() for img in imgs]
         elif pool is not None:

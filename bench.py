@@ -554,6 +554,33 @@ def unchanged_call_site(steps, warmup, cfg, cams, views, dl, dev):
     return out
 
 
+def inference_call_site(steps, warmup, P, s0, dev):
+    """train.py's inference renders (outside ``value``): render_and_export_frame
+    (train.py:506-547) under torch.no_grad() (train.py:778) -- every timestep the five fixed cameras of
+    create_extrinsic_matrices (train.py:459-503) at 1280 x 720, each call
+    ``GaussianRasterizer(raster_settings=...)(**create_render_arguments(params))``: forward only, one host
+    thread, torch's current stream, RGB colours.  One step = the five cameras; the PNG export and the
+    deformation network are outside the metric.  Msplats/s = 5 P / step time."""
+    import splat_scenes as S
+    from diff_gaussian_rasterization import GaussianRasterizer
+    params = S.synthetic_cloud(P, s0, sh_degree=-1, seed=0, device=dev)
+    cams = S.inference_cameras(device=dev)
+
+    def one(it):
+        with torch.no_grad():
+            for rs in cams:
+                GaussianRasterizer(raster_settings=rs)(**S.render_arguments(params))
+
+    host = []
+    ms = timed_steps(one, steps, warmup, dev, host)
+    out = {"workload": f"{P} Gaussians, RGB, 5 inference cameras at {S.INFERENCE_W}x{S.INFERENCE_H}, forward only "
+                       "(no_grad), create_render_arguments per render", "views_per_step": len(cams),
+           "threads": 1, "streams": "torch's current stream only", "steps": steps,
+           "host_ms_per_step_median": round(float(np.median(host)), 4)}
+    out.update(step_stats(len(cams), P, ms))
+    return out
+
+
 def c2_leg(steps, warmup, dev, nstreams=3):
     """BASELINE configs[1] (C2: 100k Gaussians, RGB, the 4 cameras of 800x800 at yaw 0/90/180/270),
     measured in the default run so the driver records it: one step = the 4 views rendered from ONE
@@ -727,6 +754,8 @@ def main():
                     help="steps timed for each call-site variant (0 = skip; N = 1, C3 only)")
     ap.add_argument("--train-steps", type=int, default=10,
                     help="steps timed for the train.py call-site legs (0 = skip; N = 1, C3 only)")
+    ap.add_argument("--inference-steps", type=int, default=20,
+                    help="steps of the inference_call_site leg (train.py's no_grad 5-camera renders; 0 = skip)")
     ap.add_argument("--unchanged-steps", type=int, default=30,
                     help="steps timed for the unchanged train.py call site (one thread, current stream, "
                          "non-leaf inputs, RGB; 0 = skip; N = 1, C3 only)")
@@ -1015,6 +1044,9 @@ def main():
     unchanged = c2 = None
     if legs and args.unchanged_steps > 0:
         unchanged = unchanged_call_site(args.unchanged_steps, 5, cfg, cams, views_of, dl, dev)
+    inference = None
+    if legs and args.inference_steps > 0:
+        inference = inference_call_site(args.inference_steps, 3, cfg.P, cfg.s0, dev)
     if legs and args.c2_steps > 0:
         c2 = c2_leg(args.c2_steps, 10, dev)
     train_site = None
@@ -1170,6 +1202,7 @@ def main():
             "host_ms_per_call": {ph: round(host[ph][0] / max(host[ph][1], 1), 5) for ph in host},
             "cpu_baseline": cpu,
             "unchanged_call_site": unchanged,
+            "inference_call_site": inference,
             "c2": c2,
             "train_call_site": train_site,
             "call_site": call_site,

@@ -165,10 +165,7 @@ typedef struct gsr_forward_info {
     int binning_layout;  /* the pair count BINNING is laid out for (>= num_rendered) */
     int speculated;      /* 1: the speculatively queued kernels stood; 0: exact path */
     unsigned long long pending;  /* ABI >= 17: nonzero = an asynchronous forward's handle */
-    /* ABI >= 17: non-NULL = the library's auxiliary stream (hipStream_t) of this device, on which the
-     * forward queued the backward's item list into the BINNING buffer (prepare_backward); the caller must
-     * not reuse that buffer before the work queued there so far is done (torch: record_stream).  The
-     * backward calls order themselves behind it. */
+    /* reserved (ABI 17-19: the item list's auxiliary stream, removed in round 5); always NULL */
     void *aux_stream;
 } gsr_forward_info;
 int gsr_forward_info_call(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,

@@ -36,6 +36,21 @@ def test_render_settings_match_reference(c):
     np.testing.assert_array_equal(m[[0, 4, 8, 12]], w2c[0])
 
 
+def test_inference_rig_matches_reference():
+    """splat_scenes.inference_rig / inference_intrinsics restate train.py's create_extrinsic_matrices and
+    render_and_export_frame's intrinsics: golden cameras 5-9 are the reference's own five, in order."""
+    rig = list(S.inference_rig().values())
+    assert len(rig) == 5
+    for i, (w2c, aspect) in enumerate(rig):
+        c = 5 + i
+        np.testing.assert_array_equal(w2c, GOLD[f"cam{c}_in_w2c"])
+        np.testing.assert_array_equal(S.inference_intrinsics(aspect), GOLD[f"cam{c}_in_K"])
+        assert tuple(int(x) for x in GOLD[f"cam{c}_in_wh"]) == (S.INFERENCE_W, S.INFERENCE_H)
+        rs = S.inference_cameras(device="cpu")[i]
+        np.testing.assert_array_equal(rs.viewmatrix.contiguous().numpy(), GOLD[f"cam{c}_viewmatrix"])
+        np.testing.assert_array_equal(rs.projmatrix.contiguous().numpy(), GOLD[f"cam{c}_projmatrix"])
+
+
 def test_render_arguments_match_reference():
     """create_render_arguments (shared.py:29-42)."""
     params = {k[len("args_in_"):]: torch.from_numpy(GOLD[k]) for k in GOLD.files if k.startswith("args_in_")}

@@ -30,18 +30,20 @@ def _torch_ssim(img1, img2):
 
 
 @pytest.mark.gpu
-def test_gpu_densify_iteration_matches_reference_composition(cuda):
+@pytest.mark.parametrize("P,W,H,f,s0", [(20000, 320, 240, 300.0, 0.02),
+                                        (1_000_000, 1920, 1080, 1600.0, 0.005)],  # C3 size
+                         ids=["20k", "C3"])
+def test_gpu_densify_iteration_matches_reference_composition(cuda, P, W, H, f, s0):
     import splat_adam
     import splat_scenes as S
     import splat_train
     from diff_gaussian_rasterization import GaussianRasterizer
-    P, W, H = 20000, 320, 240
     g = torch.Generator().manual_seed(2)
-    base = S.synthetic_cloud(P, 0.02, seed=4, device="cpu")
+    base = S.synthetic_cloud(P, s0, seed=4, device="cpu")
     base["segmentation_masks"] = (torch.rand(P, 1, generator=g) > 0.5).float().repeat(1, 3)
     base["camera_matrices"] = torch.zeros(50, 3)
     base["camera_center"] = torch.zeros(50, 3)
-    cam = S.render_settings(W, H, S.intrinsics(300.0, W, H), S.look_at(30.0, 0.3, 4.0), device=cuda)
+    cam = S.render_settings(W, H, S.intrinsics(f, W, H), S.look_at(30.0, 0.3, 4.0), device=cuda)
     view = splat_train.View(0, cam, torch.rand(3, H, W, generator=g).to(cuda),
                             (torch.rand(1, H, W, generator=g) > 0.5).float().repeat(3, 1, 1).to(cuda))
 

@@ -24,7 +24,7 @@ ap.add_argument("--no-view-streams", action="store_true")
 ap.add_argument("--steps", type=int, default=20)
 args = ap.parse_args()
 dgr.set_async_forward(not args.no_async)
-dgr.set_view_streams(not args.no_view_streams)
+# (library view streams removed in round 5)
 T = collections.defaultdict(float)
 N = collections.defaultdict(int)
 
@@ -125,7 +125,7 @@ for mode in ("idle", "busy"):
     for it in range(args.steps):
         step(10 + it, mode == "idle")
     torch.cuda.synchronize()
-    print(f"== {mode} GPU at step start (async={not args.no_async}, view_streams={not args.no_view_streams}); "
+    print(f"== {mode} GPU at step start (async={not args.no_async}); "
           f"ms per step (median of phases, totals per step)")
     for k, v in phase.items():
         v = sorted(v)

@@ -24,7 +24,7 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--P", type=int, default=1_000_000)
 args = ap.parse_args()
 dgr.set_async_forward(not args.no_async)
-dgr.set_view_streams(not args.no_view_streams)
+# (library view streams removed in round 5)
 dev = torch.device("cuda", 0)
 _C.load_library()
 base_cfg = S.CONFIGS["C3"]
@@ -71,7 +71,7 @@ for it in range(args.steps):
     step(200 + it)
 torch.cuda.synchronize()
 pr.disable()
-print(f"async={not args.no_async} view_streams={not args.no_view_streams}: wall {wall:.3f} ms/step, submission "
+print(f"async={not args.no_async}: wall {wall:.3f} ms/step, submission "
       f"{host:.3f} ms/step, host from an idle GPU {sorted(hs)[len(hs) // 2]:.3f} ms/step (median)")
 st = pstats.Stats(pr)
 st.sort_stats("tottime").print_stats(30)
