@@ -6,6 +6,7 @@
 // rasterize_points.cu glue + CudaRasterizer::Rasterizer::{forward,backward}.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -28,9 +29,6 @@
 
 using namespace gsr;
 
-#ifndef GSR_FWD_ITEMS
-#define GSR_FWD_ITEMS 1  // 0: the backward builds its item list even when the forward could (A/B)
-#endif
 
 namespace {
 
@@ -383,15 +381,20 @@ void spec_record(const SpecKey &key, uint32_t K, bool long_lists, int outcome, u
 // record (and the resolver's buffer, freed stream-ordered on the forward's stream) is dropped once
 // the caller released it and it is resolved.
 constexpr int kAsyncSlots = 4096;
-constexpr int kSlotWords = 16;  // 64 bytes: [0..3] k_bin_scan's host words, [4] the gate
-constexpr int kGateWord = 4;
+constexpr int kSlotWords = 16;  // 64 bytes: [0..3] k_bin_scan's host words, [4] the gate, [5] its timeout error
+constexpr int kGateWord = 4, kGateErrWord = 5;
+constexpr uint64_t kGateTimeoutTicks = 500000000ull;  // 5 s of s_memrealtime (100 MHz)
+// test hooks (gsr_debug_async_fault): the gate timeout of later forwards, and a delay the resolver
+// holds the next redone forward's gate closed for
+std::atomic<uint64_t> g_gate_timeout{kGateTimeoutTicks};
+std::atomic<int> g_hold_next_redo_ms{0};
 
 struct AsyncFwd {
     uint64_t id = 0;
     int dev = 0, slot = -1, T = 0;
     hipStream_t s = nullptr;
     uint32_t seq = 0, cap = 0;
-    bool prep = false, released = false;
+    bool prep = false, released = false, err_reported = false;
     SpecKey key{0, 0, 0, 0};
     FwdArgs a;                  // the launch arguments (GEOM / IMAGE / outputs carved)
     void *spec_bin = nullptr;   // the caller's BINNING, laid out for `cap`
@@ -414,14 +417,13 @@ uint32_t *g_slot_h = nullptr, *g_slot_d = nullptr;  // kAsyncSlots * kSlotWords 
 std::vector<uint8_t> g_slot_busy;
 std::vector<hipEvent_t> g_as_evpool;  // k_bin_scan events of reaped forwards
 int g_slot_next = 0;
-std::string g_async_err;  // a failed redo or gate, reported by the next call
+std::string g_async_err;  // a failed redo, or a timed-out gate whose forward was never resolved: reported
+                          // by the next forward (sticky until gsr_debug_async_fault(.., clear) or a report)
 bool g_resolver_started = false, g_resolver_stop = false;
 std::thread g_resolver;
 
 uint32_t *slot_h(int k) { return g_slot_h + (size_t)k * kSlotWords; }
 uint32_t *slot_d(int k) { return g_slot_d + (size_t)k * kSlotWords; }
-uint32_t *gate_err_h() { return g_slot_h + (size_t)kAsyncSlots * kSlotWords; }
-uint32_t *gate_err_d() { return g_slot_d + (size_t)kAsyncSlots * kSlotWords; }
 
 void resolver_main();
 
@@ -508,6 +510,8 @@ void async_reap(std::unordered_map<uint64_t, std::shared_ptr<AsyncFwd>>::iterato
     }
     if (f.ev_scan) g_as_evpool.push_back(f.ev_scan);  // a pending record may be re-recorded later
     f.ev_scan = nullptr;
+    if (f.slot >= 0 && !f.err_reported && __atomic_load_n(slot_h(f.slot) + kGateErrWord, __ATOMIC_ACQUIRE) == f.seq)
+        g_async_err = "an asynchronous forward's gate timed out (seq " + std::to_string(f.seq) + "), its outputs were not final";
     if (f.slot >= 0) g_slot_busy[f.slot] = 0;
     g_as.erase(it);
 }
@@ -524,7 +528,7 @@ int async_redo(AsyncFwd &f, hipStream_t H) {
     a.spec_ok = nullptr;
     a.spec_cap = 0;
     const size_t bin_bytes = BinningLayout((int)K, a.P).total;
-    const size_t item_bytes = (GSR_FWD_ITEMS && f.prep) ? bwd_items_bytes((int)K, f.T) : 0;
+    const size_t item_bytes = (f.prep) ? bwd_items_bytes((int)K, f.T) : 0;
     const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
     void *bin = nullptr;
     if (hipMallocAsync(&bin, bin_bytes + item_bytes + tmp_bytes, H) != hipSuccess || !bin)
@@ -534,7 +538,7 @@ int async_redo(AsyncFwd &f, hipStream_t H) {
     HIP_TRY(launch_bin_emit(a, (int)K, H));
     HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)((char *)bin + bin_bytes + item_bytes), H));
     HIP_TRY(launch_render_fwd(a, H));
-    if (GSR_FWD_ITEMS && f.prep)
+    if (f.prep)
         HIP_TRY(launch_bwd_items_raw((int)K, f.T, a.P, a.ranges, a.tile_maxc, (uint2 *)((char *)bin + bin_bytes), a.items_ws, H));
     HIP_TRY(hipStreamSynchronize(H));
     f.bin = bin;
@@ -588,6 +592,10 @@ void resolver_main() {
         lk.unlock();
         const int rc = async_redo(*next, H);
         const std::string msg = rc ? g_err : std::string();
+        if (g_hold_next_redo_ms > 0) {  // test hook: the gate stays closed a while (the wave may time out)
+            std::this_thread::sleep_for(std::chrono::milliseconds(g_hold_next_redo_ms));
+            g_hold_next_redo_ms = 0;
+        }
         __atomic_store_n(slot_h(next->slot) + kGateWord, next->seq, __ATOMIC_RELEASE);  // open the gate
         lk.lock();
         next->state = rc ? -1 : 3;
@@ -604,7 +612,7 @@ extern "C" size_t gsr_spec_binning_bytes(int P, int W, int H, int prepare_backwa
     (void)hipGetDevice(&dev);
     const uint32_t cap = spec_capacity(SpecKey{dev, P, W, H});
     if (!cap) return 0;
-    const size_t items = (GSR_FWD_ITEMS && prepare_backward) ? bwd_items_bytes((int)cap, div_up(W, kTileW) * div_up(H, kTileH)) : 0;
+    const size_t items = (prepare_backward) ? bwd_items_bytes((int)cap, div_up(W, kTileW) * div_up(H, kTileH)) : 0;
     return BinningLayout((int)cap, P).total + items;
 }
 
@@ -623,7 +631,6 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     {
         std::lock_guard<std::mutex> lk(g_as_mu);
         if (!g_async_err.empty()) return fail(GSR_ERR_HIP, "%s", g_async_err.c_str());
-        if (g_slot_h && gate_err_h()[0]) return fail(GSR_ERR_HIP, "an asynchronous forward's gate timed out (seq %u)", gate_err_h()[0]);
     }
     hipStream_t s = (hipStream_t)stream;
     FwdArgs a;
@@ -669,6 +676,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
                 af->seq = ++g_as_seq;
                 words_h = slot_h(slot);
                 words_d = slot_d(slot);
+                __atomic_store_n(words_h + kGateErrWord, 0u, __ATOMIC_RELAXED);
             }
         }
     }
@@ -699,7 +707,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         if (!af->ev_scan) HIP_TRY(hipEventCreateWithFlags(&af->ev_scan, hipEventDisableTiming | hipEventBlockingSync));
         HIP_TRY(hipEventRecord(af->ev_scan, s));
     }
-    const size_t spec_item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;
+    const size_t spec_item_bytes = (g->prepare_backward) ? bwd_items_bytes((int)cap, T) : 0;
     char *spec_bin = nullptr;
     if (cap) {  // speculative: the post-scan kernels are queued now, against the capacity
         spec_bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, BinningLayout((int)cap, a.P).total + spec_item_bytes);
@@ -710,12 +718,13 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         if (af) {  // a failed speculation holds the stream in the speculative render until it is redone
             sa.gate = words_d + kGateWord;
             sa.gate_seq = af->seq;
-            sa.gate_err = gate_err_d();
+            sa.gate_err = words_d + kGateErrWord;
+            sa.gate_timeout = g_gate_timeout;
         }
         { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(sa, 0, s)); }
         { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(sa, 0, 0, 0, nullptr, s)); }
         { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(sa, s)); }
-        if (GSR_FWD_ITEMS && g->prepare_backward) {
+        if (g->prepare_backward) {
             uint2 *items = (uint2 *)(spec_bin + BinningLayout((int)cap, a.P).total);
             Phase ph(s, "bwd_items");
             HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, s, sa.spec_ok));
@@ -777,7 +786,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     a.spec_ok = nullptr;
     // BINNING = the binning arrays, [the backward's item list], [the long-list merge buffer]
     const size_t bin_bytes = BinningLayout((int)K, a.P).total;
-    const size_t item_bytes = (GSR_FWD_ITEMS && g->prepare_backward) ? bwd_items_bytes((int)K, T) : 0;
+    const size_t item_bytes = (g->prepare_backward) ? bwd_items_bytes((int)K, T) : 0;
     const size_t tmp_bytes = n_vlong ? sizeof(uint4) * (size_t)K : 0;
     char *bin = (char *)alloc(alloc_ctx, GSR_BUF_BINNING, bin_bytes + item_bytes + tmp_bytes);
     if (!bin) return fail(GSR_ERR_ALLOC, "allocation callback failed (binning, K=%u)", K);
@@ -785,7 +794,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     { Phase ph(s, "bin_emit"); HIP_TRY(launch_bin_emit(a, (int)K, s)); }
     { Phase ph(s, "tile_sort"); HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)(bin + bin_bytes + item_bytes), s)); }
     { Phase ph(s, "render_fwd"); HIP_TRY(launch_render_fwd(a, s)); }
-    if (GSR_FWD_ITEMS && g->prepare_backward) {  // the backward's item list, built here, off its critical path
+    if (g->prepare_backward) {  // the backward's item list, built here, off its critical path
         uint2 *items = (uint2 *)(bin + bin_bytes);
         Phase ph(s, "bwd_items");
         HIP_TRY(launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, s));
@@ -863,6 +872,13 @@ int gsr_forward_resolve(unsigned long long handle, gsr_forward_resolution *out) 
         g_as_done.wait(lk);
     }
     if (f->state < 0) return fail(GSR_ERR_HIP, "asynchronous forward %llu failed: %s", handle, f->err.c_str());
+    // a gate the render abandoned (timeout) before the redo opened it: everything the caller queued after
+    // the forward ran on outputs that were not final -- this forward's resolution (the step's backward) fails
+    if (__atomic_load_n(slot_h(f->slot) + kGateErrWord, __ATOMIC_ACQUIRE) == f->seq) {
+        f->err_reported = true;
+        return fail(GSR_ERR_HIP, "asynchronous forward %llu: its gate timed out before the redo opened it; the outputs "
+                    "the caller used after the forward were not final", handle);
+    }
     out->num_rendered = (int)f->K;
     out->binning_layout = f->layout;
     out->binning = f->bin;
@@ -925,6 +941,14 @@ int gsr_spec_stats(int *hits, int *misses, int reset) {
     return GSR_OK;
 }
 
+int gsr_debug_async_fault(int hold_next_redo_ms, int gate_timeout_ms, int clear) {
+    std::lock_guard<std::mutex> lk(g_as_mu);
+    g_hold_next_redo_ms = hold_next_redo_ms > 0 ? hold_next_redo_ms : 0;
+    g_gate_timeout = gate_timeout_ms > 0 ? (uint64_t)gate_timeout_ms * 100000ull : kGateTimeoutTicks;
+    if (clear) g_async_err.clear();
+    return GSR_OK;
+}
+
 int gsr_spec_keys(void) {
     std::lock_guard<std::mutex> lk(g_spec_mu);
     return (int)g_spec.size();
@@ -976,7 +1000,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     if (!scr) return fail(GSR_ERR_ALLOC, "allocation callback failed (scratch)");
     a.part = (float4 *)(scr + SL.part);
     a.max_items = (uint32_t)max_bwd_items(num_rendered, a.gx * a.gy);
-    if (GSR_FWD_ITEMS && g->prepare_backward) {  // built by the forward, after the binning arrays
+    if (g->prepare_backward) {  // built by the forward, after the binning arrays
         a.items = (uint2 *)((char *)binning + BinningLayout(layout, a.P).total);
     } else {
         a.items = (uint2 *)(scr + SL.items);

@@ -21,63 +21,7 @@ namespace gsr {
 __device__ uint64_t *g_trace_bwd;
 #endif
 
-// The backward's work items in longest-first order, built by one block from the forward's tile
-// ranges and per-quarter maxima: items bucketed by exact cost (bwd_item_cost + a fixed per-item
-// start-up cost, kOrderBuckets buckets, descending), so the hardware's in-order dispatch of the
-// launch's residency rounds is a greedy LPT schedule.  Item order inside a bucket follows LDS
-// atomics (scheduling only: every item writes its own slots).  items[0].x = the item count.
 constexpr uint32_t kItemStartCost = 64;  // init loads + first gathers, in (pair, quarter) steps
-__global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restrict__ ranges,
-                                                    const uint32_t *__restrict__ tile_maxc,
-                                                    uint2 *__restrict__ items, const uint32_t *__restrict__ spec_ok,
-                                                    int ks) {
-    __shared__ uint32_t s_hist[kOrderBuckets];
-    __shared__ uint32_t s_red[16];
-    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
-    for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) s_hist[b] = 0;
-    const uint32_t kMaxCost = (4u << ks) + kItemStartCost;
-    const uint32_t kShift = kMaxCost >= (uint32_t)kOrderBuckets ? 32 - __builtin_clz(kMaxCost / kOrderBuckets) : 0;
-    auto bucket = [kShift](uint32_t cost) { return (uint32_t)kOrderBuckets - 1u - min(cost >> kShift, (uint32_t)kOrderBuckets - 1u); };
-    __syncthreads();
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int t0 = 0; t0 < T; t0 += kScanRegs * (int)blockDim.x) {  // kScanRegs tiles' loads in flight
-            uint32_t nn[kScanRegs];
-            uint4 mq[kScanRegs];
-#pragma unroll
-            for (int i = 0; i < kScanRegs; ++i) {
-                const int t = t0 + i * (int)blockDim.x + (int)threadIdx.x;
-                const uint2 rg = t < T ? ranges[t] : make_uint2(0, 0);
-                mq[i] = t < T ? reinterpret_cast<const uint4 *>(tile_maxc)[t] : make_uint4(0, 0, 0, 0);
-                nn[i] = rg.y - rg.x;
-            }
-#pragma unroll
-            for (int i = 0; i < kScanRegs; ++i) {
-                const uint32_t t = (uint32_t)(t0 + i * (int)blockDim.x + (int)threadIdx.x);
-                const uint32_t J = bwd_item_count(nn[i], mq[i], ks), Z = bwd_zero_items(nn[i], mq[i]);
-                for (uint32_t j = 0; j < J + Z; ++j) {
-                    const uint32_t cost = j < J ? bwd_item_cost(j, mq[i], ks) + kItemStartCost : kItemStartCost;
-                    const uint32_t b = bucket(cost);
-                    if (pass == 0) atomicAdd(&s_hist[b], 1u);
-                    else items[1 + atomicAdd(&s_hist[b], 1u)] = make_uint2(t, j < J ? j : kZeroItem | (j - J));
-                }
-            }
-        }
-        if (pass == 0) {
-            __syncthreads();
-            uint32_t carry = 0;
-            for (int base = 0; base < kOrderBuckets; base += blockDim.x) {
-                const int b = base + threadIdx.x;
-                const uint32_t h = b < kOrderBuckets ? s_hist[b] : 0;
-                uint32_t tot;
-                const uint32_t ex = block_excl_scan_u32(h, s_red, &tot) + carry;
-                if (b < kOrderBuckets) s_hist[b] = ex;
-                carry += tot;
-            }
-            if (threadIdx.x == 0) items[0] = make_uint2(carry, 0u);
-            __syncthreads();
-        }
-    }
-}
 
 // The same item list built over the whole chip (the single block above runs on ONE CU: ~30 us at C3,
 // 21 at C2, on the view's critical path).  k_items_count: one thread per tile counts its items per cost
@@ -86,9 +30,6 @@ __global__ __launch_bounds__(1024) void k_bwd_items(int T, const uint2 *__restri
 // scan, descending cost).  k_items_emit: each block counts its tiles' items again, reserves its run in
 // every bucket with one global atomic, and hands out the slots from LDS.  Order inside a bucket
 // follows the atomics (scheduling only).
-#ifndef GSR_ITEMS_MB
-#define GSR_ITEMS_MB 1  // 0: the single-block k_bwd_items
-#endif
 constexpr int kItemsBlock = 256;  // tiles (threads) per block
 struct ItemBucket {  // item cost -> LPT bucket (descending cost) for segments of 2^ks entries
     uint32_t shift;
@@ -212,10 +153,8 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
     d[2] = F3{r6, r7, r8};
 }
 
-#ifndef GSR_BWD_WPE
-#define GSR_BWD_WPE 5  // waves per SIMD the register budget is held to
-#endif
-#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_BWD_WPE, 8)))
+// the register budget of 5 waves per SIMD (96 VGPRs; 6 waves spilled and ran slower)
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
 constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
 
 // ---- the pair reduction ---------------------------------------------------------------------------
@@ -683,28 +622,14 @@ template <int MC> constexpr int kRecStageF4 = 3 * kRecChunk<MC>;  // float4 per 
 // 16-byte aligned address at or below its first float: (kRecF cb) & 3 floats of lead-in.
 __host__ __device__ constexpr int rec_chunk_f4(int C) { return (kRecF * C + 3 + 3) / 4; }
 // A lane's records [lo, hi) of a chunk staged at `sf` (record cb at sf[0]), added into acc in
-// emission order.  GSR_REC_UNROLL records per trip with their LDS reads issued together; past hi the
-// slots read as -0, the exact identity of fp32 addition, so the sums are bitwise those of a
-// one-record-per-trip walk (2 and 4 per trip measured slower: DESIGN 2.5).
-#ifndef GSR_REC_UNROLL
-#define GSR_REC_UNROLL 1
-#endif
+// emission order, one record per trip (2 and 4 per trip with their LDS reads issued together measured
+// slower: DESIGN 2.5).
 __device__ inline void add_chunk_records(const float *sf, uint32_t cb, uint32_t lo, uint32_t hi,
                                          float (&acc)[kPartial]) {
-    constexpr int U = GSR_REC_UNROLL;
-    for (uint32_t e = lo; e < hi; e += U) {
-        float r[U][kPartial];
+    for (uint32_t e = lo; e < hi; ++e) {
+        const float *p = sf + kRecF * (e - cb);
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float *p = sf + kRecF * (e + u - cb);
-            const bool in = U == 1 || e + u < hi;
-#pragma unroll
-            for (int k = 0; k < kPartial; ++k) r[u][k] = in ? p[k] : -0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-            for (int k = 0; k < kPartial; ++k) acc[k] += r[u][k];
+        for (int k = 0; k < kPartial; ++k) acc[k] += p[k];
     }
 }
 
@@ -1035,14 +960,7 @@ __global__ __launch_bounds__(256) void k_sum_records(int P, const uint32_t *__re
 // Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
 // read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
-#ifndef GSR_MV_WPE
-#define GSR_MV_WPE 0  // waves per SIMD the register budget is held to (0: the compiler's choice)
-#endif
-#if GSR_MV_WPE
-#define GSR_MV_ATTR __attribute__((amdgpu_waves_per_eu(GSR_MV_WPE, 8)))
-#else
-#define GSR_MV_ATTR
-#endif
+#define GSR_MV_ATTR  // (the compiler's register budget: 4 waves/SIMD spilled)
 template <int MC>
 constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_stride(MC) + 3) & ~size_t(3)) : 0; }
 template <int MC>
@@ -1254,13 +1172,9 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
                                 uint32_t *ws, hipStream_t s, const uint32_t *spec_ok) {
     if (K == 0) return hipSuccess;
-    if (GSR_ITEMS_MB) {
-        const int nb = div_up(T, kItemsBlock);
-        k_items_count<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
-        k_items_emit<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
-    } else {
-        k_bwd_items<<<1, 1024, 0, s>>>(T, ranges, tile_maxc, items, spec_ok, seg_log2(P));
-    }
+    const int nb = div_up(T, kItemsBlock);
+    k_items_count<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
+    k_items_emit<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
     return hipGetLastError();
 }
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {

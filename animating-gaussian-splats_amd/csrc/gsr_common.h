@@ -56,10 +56,7 @@ struct GeomLayout {
 };
 
 // Binning work decomposition over Gaussians: NB chunks of CH Gaussians (CH multiple of 256).
-#ifndef GSR_BIN_THREADS
-#define GSR_BIN_THREADS 1024
-#endif
-constexpr int kBinThreads = GSR_BIN_THREADS;  // threads per binning block (one chunk of CH Gaussians)
+constexpr int kBinThreads = 1024;  // threads per binning block (one chunk of CH Gaussians; 256 / 512 measured)
 // Tile histogram kept in LDS when T * 4 B fits in 64 KiB; larger tile grids (e.g. 4K frames)
 // count straight into global memory.
 constexpr int kMaxLdsTiles = 16384;
@@ -80,13 +77,7 @@ struct BinGrid {
 // (front colour, transmittance) before entry kSeg, 2 kSeg, ... of its tile: the state a segment's
 // reverse walk starts from.  A power of two >= the forward's 64-entry batch (k_render_fwd tests
 // boundaries with a mask).  256: measured against 128 / 512 / 1024 (tools/ab_variants.sh).
-#ifndef GSR_FWD_PREFETCH
-#define GSR_FWD_PREFETCH 1  // k_render_fwd loads each batch's records during the previous blend
-#endif
-#ifndef GSR_KSEG
-#define GSR_KSEG 256
-#endif
-constexpr int kSeg = GSR_KSEG;  // the longest segment
+constexpr int kSeg = 256;  // the longest segment
 static_assert(kSeg >= 64 && (kSeg & (kSeg - 1)) == 0, "kSeg: a power of two, >= the forward's 64-entry batch");
 constexpr int kSegLog2Max = __builtin_ctz(kSeg), kSegLog2Min = 6;
 // The segment length of a cloud of P Gaussians, log2 (fixed before the pair count is known: the
@@ -447,14 +438,7 @@ struct CamStrides { int v0, v1, p0, p1, c0; };
 // The camera inputs are read through the constant address space: their addresses are wave-uniform
 // and no kernel writes them, so these become scalar loads into SGPRs (as plain global pointers next to
 // the kernels' unrestricted output pointers, they were 35 per-lane vector loads into VGPRs per view).
-#ifndef GSR_CAM_SLOAD
-#define GSR_CAM_SLOAD 1
-#endif
-#if GSR_CAM_SLOAD
 typedef const __attribute__((address_space(4))) float *cam_ptr;
-#else
-typedef const float *cam_ptr;
-#endif
 __device__ inline void load_mat16(const float *__restrict__ m, int s0, int s1, float (&out)[16]) {
     const cam_ptr c = (cam_ptr)m;
 #pragma unroll

@@ -639,18 +639,27 @@ __device__ inline void wave_sort_stages(uint64_t (&k)[R], uint32_t (&v)[R], int 
     }
 }
 
+// LDS slot of sorted element i: one pad element after every 16, so that the 16 lanes of a register
+// row -- elements l R + r, l = 0..15 -- land on 16 distinct 8-byte bank pairs (unpadded, lanes l,
+// l + 16 / R, ... collide: a 4-way conflict at R = 4).  A lane's R elements (R | 16) stay adjacent, so
+// its stores and the exchange partner's loads (i ^ j, j a multiple of 64 R) are one address plus
+// immediate offsets, and consecutive elements stay conflict-free for the readers of the sorted run.
+__device__ inline uint32_t sort_slot(uint32_t i) { return i + (i >> 4); }
+constexpr int sort_slots(int n) { return n + n / 16; }
+
 // One cross-wave compare-exchange stage (distance J >= 64 R) of merge size KK through LDS.
 template <int R>
 __device__ inline void block_xchg_stage(uint64_t (&k)[R], uint32_t (&v)[R], uint32_t ibase, int kk, int j,
                                         uint64_t *s_key, uint32_t *s_val) {
+    const uint32_t sb = sort_slot(ibase), qb = sort_slot(ibase ^ (uint32_t)j);
 #pragma unroll
-    for (int r = 0; r < R; ++r) { s_key[ibase + r] = k[r]; s_val[ibase + r] = v[r]; }
+    for (int r = 0; r < R; ++r) { s_key[sb + r] = k[r]; s_val[sb + r] = v[r]; }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const uint32_t i = ibase + r, q = i ^ (uint32_t)j;
-        const uint64_t pk = s_key[q];
-        const uint32_t pv = s_val[q];
+        const uint32_t i = ibase + r;
+        const uint64_t pk = s_key[qb + r];
+        const uint32_t pv = s_val[qb + r];
         const bool take_min = ((i & j) == 0) == ((i & kk) == 0);
         const bool mine = (k[r] < pk) == take_min;
         k[r] = mine ? k[r] : pk;
@@ -661,9 +670,9 @@ __device__ inline void block_xchg_stage(uint64_t (&k)[R], uint32_t (&v)[R], uint
 
 // Sort one tile's n <= 64 R NW (key, emission) pairs with the block's NW waves: each wave sorts its
 // 64 R-element segment in registers (DPP / swizzle / permlane exchanges), then every cross-wave
-// merge level exchanges through LDS for distances >= 64 R and finishes in registers.  Leaves the
-// sorted keys in s_key[0, n) and emissions in s_val[0, n).  Keys are (depth_bits << 32 | index),
-// unique inside a tile.
+// merge level exchanges through LDS for distances >= 64 R and finishes in registers.  Leaves sorted
+// element i (key, emission) at s_key / s_val[sort_slot(i)], i < n (arrays of sort_slots(64 R NW)).  Keys are
+// (depth_bits << 32 | index), unique inside a tile.
 template <int R, int NW>
 __device__ inline void block_sort_tile(int n, uint32_t start, const uint4 *__restrict__ pairs, uint64_t *s_key,
                                        uint32_t *s_val) {
@@ -684,8 +693,9 @@ __device__ inline void block_sort_tile(int n, uint32_t start, const uint4 *__res
         for (uint32_t j = kk >> 1; j >= (uint32_t)SEG; j >>= 1) block_xchg_stage<R>(k, v, ibase, kk, j, s_key, s_val);
         wave_merge_stages<R, SEG / 2>(k, v, lane, gbase, kk);
     }
+    const uint32_t sb = sort_slot(ibase);
 #pragma unroll
-    for (int r = 0; r < R; ++r) { s_key[ibase + r] = k[r]; s_val[ibase + r] = v[r]; }
+    for (int r = 0; r < R; ++r) { s_key[sb + r] = k[r]; s_val[sb + r] = v[r]; }
     __syncthreads();
 }
 
@@ -700,8 +710,8 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
                                                     uint32_t *__restrict__ point_list,
                                                     uint32_t *__restrict__ slot_emit, uint32_t nlist,
                                                     const uint32_t *__restrict__ spec_ok) {
-    __shared__ uint64_t s_keys[kSortCap];
-    __shared__ uint32_t s_vals[kSortCap];
+    __shared__ uint64_t s_keys[sort_slots(kSortCap)];
+    __shared__ uint32_t s_vals[sort_slots(kSortCap)];
     if (spec_ok) {
         if (*spec_ok == 0u) return;
         nlist = spec_ok[1];  // meta[2]: tiles of kFwdSortCap < n <= kSortCap pairs
@@ -714,8 +724,9 @@ __global__ __launch_bounds__(512) void k_tile_sort(int gx, const uint32_t *__res
         if (n <= 4 * 64 * 8) block_sort_tile<4, 8>(n, rg.x, pairs, s_keys, s_vals);
         else block_sort_tile<8, 8>(n, rg.x, pairs, s_keys, s_vals);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            point_list[rg.x + i] = (uint32_t)s_keys[i];
-            slot_emit[rg.x + i] = s_vals[i];
+            const uint32_t sl = sort_slot((uint32_t)i);
+            point_list[rg.x + i] = (uint32_t)s_keys[sl];
+            slot_emit[rg.x + i] = s_vals[sl];
         }
         __syncthreads();  // the LDS keys are reused by the block's next list
     }
@@ -737,8 +748,8 @@ __device__ inline uint4 key_record(uint64_t k, uint32_t emit) {
 
 __global__ __launch_bounds__(512) void k_chunk_sort(int T, const uint32_t *__restrict__ lists,
                                                      const uint2 *__restrict__ ranges, uint4 *__restrict__ pairs) {
-    __shared__ uint64_t s_keys[kSortCap];
-    __shared__ uint32_t s_vals[kSortCap];
+    __shared__ uint64_t s_keys[sort_slots(kSortCap)];
+    __shared__ uint32_t s_vals[sort_slots(kSortCap)];
     const int tile = (int)lists[T - 1 - (int)blockIdx.y];  // long tiles are listed from the end
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
@@ -746,7 +757,10 @@ __global__ __launch_bounds__(512) void k_chunk_sort(int T, const uint32_t *__res
     if (c0 >= n) return;
     const int m = min(kSortCap, n - c0);
     block_sort_tile<8, 8>(m, rg.x + c0, pairs, s_keys, s_vals);
-    for (int i = threadIdx.x; i < m; i += blockDim.x) pairs[rg.x + c0 + i] = key_record(s_keys[i], s_vals[i]);
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const uint32_t sl = sort_slot((uint32_t)i);
+        pairs[rg.x + c0 + i] = key_record(s_keys[sl], s_vals[sl]);
+    }
 }
 
 // Merge-path split of diagonal d between sorted runs a (length la) and b (length lb): the number of
@@ -828,22 +842,19 @@ __global__ __launch_bounds__(512) void k_merge_pass(int T, const uint32_t *__res
 // render record and tests it against quarter q = pixel rows 4q..4q+3 with a conservative ellipse
 // bound), then wave q blends its 16x4 quarter (one pixel per lane) over the entries whose bit q is
 // set; saturated quarters skip their evaluations and the walk ends when all four are saturated.
-#ifndef GSR_FWD_Q8
-#define GSR_FWD_Q8 1  // 8x8 quarters per wave (0: 16x4 strips, the backward's quarters)
-#endif
 // Asynchronous forwards (gsr_forward_async): when k_bin_scan found the speculative capacity too
 // small (spec_ok == 0: the queued kernels return at once), the speculative k_render_fwd's first wave
 // holds the stream until the library's resolver thread has redone the post-scan kernels exactly on its
 // own stream and published `seq` in the forward's gate word (host-mapped) -- everything the caller
 // queues after the forward is ordered behind it.  When the speculation stood nothing waits.  A gate that
-// never opens (the resolver died or is stuck) is abandoned after kGateTimeoutTicks with an error word
-// set, so a failure cannot hang the device.
-constexpr uint64_t kGateTimeoutTicks = 500000000ull;  // s_memrealtime runs at 100 MHz: 5 s
-__device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *err) {
+// never opens (the resolver died or is stuck) is abandoned after `timeout` ticks (5 s by default) with
+// the forward's error word set, so a failure cannot hang the device; the host then fails that forward's
+// resolution (gsr_forward_resolve), i.e. the backward of the step whose outputs are not final.
+__device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *err, uint64_t timeout) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while ((int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
         __builtin_amdgcn_s_sleep(100);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
             if (threadIdx.x == 0) __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
@@ -858,12 +869,15 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
     float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok,
-    int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err) {
-    __shared__ uint64_t s_key[kFwdSortCap];
+    int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err, uint64_t gate_timeout) {
+    __shared__ uint64_t s_key[sort_slots(kFwdSortCap)];
     __shared__ union {
-        uint32_t val[kFwdSortCap];  // sort payload (emission index), until written out
+        uint32_t val[sort_slots(kFwdSortCap)];  // sort payload (emission index), until written out
         struct {
-            float4 rec[3][64];      // then: the staged batch of 64 render records
+            // then: the staged batch of 64 render records, part q of entry e at rec[q][e]; rows padded by
+            // 2 float4 so that the staging stores of one entry's 3 parts (lanes 4e + q) fall in distinct
+            // banks (unpadded the rows are 1 KiB apart: a 3-way conflict in every 8-lane group)
+            float4 rec[3][66];
             uint32_t q[64];         // and their quarter masks
         } st;
     } s_u;
@@ -872,7 +886,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     if (spec_ok && *spec_ok == 0u) {  // speculative launch whose capacity failed: redone by the host
-        if (gate && blockIdx.x == 0 && threadIdx.x < 64) gate_wait(gate, gate_seq, gate_err);  // (asynchronous)
+        if (gate && blockIdx.x == 0 && threadIdx.x < 64) gate_wait(gate, gate_seq, gate_err, gate_timeout);  // (asynchronous)
         return;
     }
     const int tile = (int)tile_order[blockIdx.x];
@@ -884,20 +898,17 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, pairs, s_key, s_u.val);
         else block_sort_tile<4, 4>(n, rg.x, pairs, s_key, s_u.val);
         for (int i = threadIdx.x; i < n; i += 256) {
-            point_list[rg.x + i] = (uint32_t)s_key[i];
-            slot_emit[rg.x + i] = s_u.val[i];
+            const uint32_t sl = sort_slot((uint32_t)i);
+            point_list[rg.x + i] = (uint32_t)s_key[sl];
+            slot_emit[rg.x + i] = s_u.val[sl];
         }
     }
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int tx = tile % gx, ty = tile / gx;
-#if GSR_FWD_Q8
     // wave q blends the 8x8 quarter (8 (q & 1), 8 (q >> 1)) of the tile: a compact footprint crosses
     // fewer quarters than a 16x4 strip (tools/contrib_stats.py: 1.54 vs 1.73 evaluated quarters per
     // list entry at C3)
     const int lx = 8 * (wv & 1) + (lane & 7), ly = 8 * (wv >> 1) + (lane >> 3);
-#else
-    const int lx = lane & 15, ly = 4 * wv + (lane >> 4);  // 16x4 strips
-#endif
     const int px = tx * kTileW + lx;
     const int py = ty * kTileH + ly;
     const float pfx = (float)px, pfy = (float)py;
@@ -905,13 +916,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const int bslot = 64 * (ly >> 2) + 16 * (ly & 3) + lx;
     // staging role: thread 4e + q handles entry e of the batch against quarter q
     const int se = threadIdx.x >> 2, sq = threadIdx.x & 3;
-#if GSR_FWD_Q8
     const float qx0 = (float)(tx * kTileW + 8 * (sq & 1)), qy0 = (float)(ty * kTileH + 8 * (sq >> 1));
     constexpr int kQW = 8, kQH = 8;
-#else
-    const float qx0 = (float)(tx * kTileW), qy0 = (float)(ty * kTileH + 4 * sq);
-    constexpr int kQW = kTileW, kQH = 4;
-#endif
     const bool inside = px < W && py < H;
     // The pixel's alpha threshold: 1/255 while it blends, 2 (above any alpha <= 0.99) once it is done
     // (outside the image, or saturated): a finished pixel fails the same compare instead of carrying
@@ -924,25 +930,23 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     if (__ballot(thr < kThrDone) && lane == 0) atomicOr(&s_live, 1u << wv);
     float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
     uint32_t last = 0;
-#if GSR_FWD_PREFETCH
     // entry se of the NEXT batch: its render record halves (x, y, conic; colour) in registers, loaded
     // one batch ahead so the gathers' latency hides behind the current batch's blend
     float4 pa = make_float4(0.f, 0.f, 0.f, 0.f), pb = pa, pr = pa;
     bool pv = false;
-#define GSR_FWD_FETCH(bse)                                                                         \
+#define FETCH_BATCH(bse)                                                                           \
     do {                                                                                           \
         const int idx_ = (bse) + se;                                                               \
         pv = idx_ < n;                                                                             \
         if (pv) {                                                                                  \
-            const uint32_t g_ = sorted_here ? (uint32_t)s_key[idx_] : point_list[rg.x + idx_];      \
+            const uint32_t g_ = sorted_here ? (uint32_t)s_key[sort_slot(idx_)] : point_list[rg.x + idx_]; \
             const float4 *r_ = rec + (size_t)kRecF4 * g_;                                          \
             pa = r_[0];                                                                            \
             pb = r_[1];                                                                            \
             pr = r_[sq < 3 ? sq : 2];                                                              \
         }                                                                                          \
     } while (0)
-    GSR_FWD_FETCH(0);
-#endif
+    FETCH_BATCH(0);
     for (int base = 0; base < n; base += 64) {
         lds_barrier();  // previous batch fully consumed; s_live up to date
         const uint32_t live = s_live;
@@ -952,13 +956,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         // every boundary below its pixels' last contributor (done pixels store their final state)
         // (8x8 quarters: every quarter stores while any is live -- the backward reads whole 16x4 strips,
         // which span two quarters; a finished pixel's state is its final one)
-        if (base > 0 && (base & ((1 << ks) - 1)) == 0 && (GSR_FWD_Q8 || ((live >> wv) & 1u))) {
+        if (base > 0 && (base & ((1 << ks) - 1)) == 0) {
             const size_t b = (size_t)seg_off[tile] + ((uint32_t)base >> ks) - 1u;
             seg_state[b * kTilePix + bslot] = make_float4(C0, C1, C2, Tt);
         }
         // ---- stage the batch (block-wide) ----
         bool hit = false;
-#if GSR_FWD_PREFETCH
         {   // this batch's records were loaded during the previous batch's blend
             const float4 a = pa, b = pb;
             if (pv) {
@@ -966,18 +969,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
                 hit = ((live >> sq) & 1u) &&
                       !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kQW - 1), qy0 + (kQH - 1));
             }
-            GSR_FWD_FETCH(base + 64);
+            FETCH_BATCH(base + 64);
         }
-#else
-        const int idx = base + se;
-        if (idx < n) {
-            const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
-            const float4 a = rec[(size_t)kRecF4 * g], b = rec[(size_t)kRecF4 * g + 1];
-            if (sq < 3) s_u.st.rec[sq][se] = rec[(size_t)kRecF4 * g + sq];
-            hit = ((live >> sq) & 1u) &&
-                  !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx0 + (kQW - 1), qy0 + (kQH - 1));
-        }
-#endif
         // combine the 4 quarter bits of entry se (lanes 4e..4e+3 of this wave) with DPP
         uint32_t bits = hit ? (1u << sq) : 0u;
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xF, 0xF, false);  // xor 1
@@ -1012,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
                 const bool nr = thr < kThrDone && near_threshold(e.alpha);
                 if (__ballot(nr) && nr) {
                     const int idx = base + j;
-                    const uint32_t g = sorted_here ? (uint32_t)s_key[idx] : point_list[rg.x + idx];
+                    const uint32_t g = sorted_here ? (uint32_t)s_key[sort_slot(idx)] : point_list[rg.x + idx];
                     const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
                     e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
                 }
@@ -1032,7 +1025,6 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         out_color[2 * H * W + pid] = C2 + Tt * bg[2];
         out_depth[pid] = Dp;
     }
-#if GSR_FWD_Q8
     // per 16x4 strip maximum of n_contrib (the backward's quarters): rows 4k..4k+3 = half of the lanes of
     // two waves; lanes (lane >> 3) < 4 hold strip 2 (wv >> 1), the others strip 2 (wv >> 1) + 1
     uint32_t mx = last;
@@ -1044,12 +1036,6 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     if ((lane & 31) == 0) atomicMax(&s_u.st.q[2 * (wv >> 1) + (lane >> 5)], mx);
     lds_barrier();  // the quarter maxima: no-return LDS atomics
     if (threadIdx.x < 4) tile_maxc[4 * tile + threadIdx.x] = s_u.st.q[threadIdx.x];
-#else
-    uint32_t mx = last;
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
-    if (lane == 0) tile_maxc[4 * tile + wv] = mx;
-#endif
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
 #endif
@@ -1173,7 +1159,7 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     k<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                         a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
                         a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
-                        a.gate_err);
+                        a.gate_err, a.gate_timeout);
     return hipGetLastError();
 }
 

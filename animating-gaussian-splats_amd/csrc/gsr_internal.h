@@ -29,8 +29,9 @@ struct FwdArgs {
     uint32_t spec_cap; const uint32_t *spec_ok;
     uint32_t spec_sort_blocks;  // grid of the speculative k_tile_sort (<= kSpecSortBlocks; 0: that bound)
     // asynchronous forward (gsr_forward_async): the gate word the speculative render's first wave waits
-    // on when the speculation failed, the value that opens it, and the timeout error word
-    const uint32_t *gate; uint32_t gate_seq; uint32_t *gate_err;
+    // on when the speculation failed, the value that opens it, the forward's timeout error word (set to
+    // gate_seq when the gate is abandoned) and the timeout (s_memrealtime ticks, 100 MHz)
+    const uint32_t *gate; uint32_t gate_seq; uint32_t *gate_err; uint64_t gate_timeout;
     // exact-threshold mode (gsr_set_exact_thresholds): near-threshold blend weights re-evaluated
     int exact;
 };

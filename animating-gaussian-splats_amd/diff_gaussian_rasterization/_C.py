@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "gsr_grad_fence", "gsr_backward_render", "gsr_backward_gaussians", "gsr_backward_items_bytes",
     "gsr_forward_info_call", "gsr_spec_stats", "gsr_sums_bytes", "gsr_prealloc_alloc", "gsr_spec_binning_bytes",
     "gsr_forward_async", "gsr_forward_resolve", "gsr_forward_release", "gsr_forward_query", "gsr_async_stats",
-    "gsr_spec_keys", "gsr_async_shutdown", "gsr_set_exact_thresholds",
+    "gsr_spec_keys", "gsr_async_shutdown", "gsr_debug_async_fault", "gsr_set_exact_thresholds",
 )
 
 
@@ -130,6 +130,8 @@ def load_library():
     L.gsr_async_stats.argtypes = [ctypes.POINTER(i), ctypes.POINTER(i)]
     L.gsr_async_shutdown.restype = i
     L.gsr_async_shutdown.argtypes = []
+    L.gsr_debug_async_fault.restype = i
+    L.gsr_debug_async_fault.argtypes = [i, i, i]
     import atexit
     atexit.register(L.gsr_async_shutdown)  # the resolver thread stops before the HIP runtime goes
     L.gsr_backward.restype = i
@@ -186,7 +188,7 @@ def load_library():
     return L
 
 
-ABI_VERSION = 19  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 20  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
@@ -496,6 +498,12 @@ class AsyncForward:
 def _release_async(handle):
     if _lib is not None:
         _lib.gsr_forward_release(handle)
+
+
+def debug_async_fault(hold_next_redo_ms=0, gate_timeout_ms=0, clear=False):
+    """Test hook (include/gsr.h gsr_debug_async_fault): hold the next redone asynchronous forward's gate
+    closed for `hold_next_redo_ms`, time gates out after `gate_timeout_ms` (0: the default 5 s)."""
+    _check(load_library().gsr_debug_async_fault(int(hold_next_redo_ms), int(gate_timeout_ms), int(bool(clear))))
 
 
 def async_stats():

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 19
+#define GSR_ABI_VERSION 20
 
 enum gsr_status {
     GSR_OK = 0,
@@ -199,6 +199,11 @@ typedef struct gsr_forward_resolution {
 } gsr_forward_resolution;
 int gsr_forward_async(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn alloc, void *alloc_ctx,
                       float *out_color, float *out_depth, int *out_radii, gsr_forward_info *info, void *stream);
+/* Waits until the forward's pair count is known (and a failed speculation redone).  Fails (GSR_ERR_HIP)
+ * when the forward failed, or when its render abandoned the gate (a 5 s timeout) before the redo opened
+ * it -- the caller's work queued after the forward then ran on outputs that were not final, so the step
+ * must not go on (the binding raises in that step's backward).  A timed-out forward released without a
+ * resolution makes the next forward fail instead. */
 int gsr_forward_resolve(unsigned long long handle, gsr_forward_resolution *out);
 int gsr_forward_release(unsigned long long handle);
 /* 1: gsr_forward_resolve would return without waiting; 0: not yet; -1: unknown handle. */
@@ -208,6 +213,10 @@ int gsr_async_stats(int *calls, int *pending);
 /* Stops the resolver thread once it has no redo in flight (call at process exit, before the HIP
  * runtime is torn down; a later asynchronous forward starts it again). */
 int gsr_async_shutdown(void);
+/* Test hook for the asynchronous forward's failure path: the resolver keeps the NEXT redone forward's
+ * gate closed for hold_next_redo_ms (0: no delay), later forwards' gates time out after gate_timeout_ms
+ * (<= 0: the default 5 s); clear != 0 also drops a pending sticky error (see gsr_forward_resolve). */
+int gsr_debug_async_fault(int hold_next_redo_ms, int gate_timeout_ms, int clear);
 
 /* Backward of gsr_forward given dL/d(color) (3,H,W).  dL_ddepth is accepted and ignored: the
  * reference discards the depth output (train.py:355-361, densify.py:120-126) and its -w-depth

@@ -272,3 +272,43 @@ def test_speculative_render_half_bitwise(cuda, miss):
     assert ref[1].keys() == got[1].keys()
     for k in ref[1]:
         assert torch.equal(ref[1][k], got[1][k]), k
+
+
+@pytest.mark.parametrize("shape", ["call", "autograd"])
+def test_gate_timeout_fails_that_steps_backward(cuda, shape):
+    """A failed speculation whose redo the resolver holds back longer than the gate's timeout (test hook
+    gsr_debug_async_fault: 300 ms hold, 20 ms timeout): the speculative render abandons the gate, the
+    work queued after the forward runs on outputs that are not final -- and that SAME step must fail:
+    the forward's resolution (at the step's backward) raises.  Afterwards the library recovers (no
+    sticky error): the next asynchronous step equals the blocking one bitwise."""
+    P, W, H = 60_000, 640, 480
+    a = _cloud(cuda, P)
+    dense = dict(a, scales=a["scales"] * 4.0)  # past the sparse cloud's capacity (see above)
+    cam = S.render_settings(W, H, S.intrinsics(500.0, W, H), S.look_at(30, 0.2, 9.0), device=cuda, sh_degree=3)
+    dl = S.upstream_grad(H, W, device=cuda)
+    _C.speculation_stats(reset=True)
+    _run(a, cam, "exact", dl)  # history: the sparse cloud
+    _C.debug_async_fault(hold_next_redo_ms=300, gate_timeout_ms=20)
+    try:
+        if shape == "call":
+            info, out = _forward(dense, cam, "async")
+            torch.cuda.synchronize()  # the stream passes the abandoned gate (20 ms)
+            with pytest.raises(RuntimeError, match="gate timed out"):
+                _backward(dense, cam, out, info, dl)
+            del info, out
+        else:
+            leaves = {k: v.detach().clone().requires_grad_(True) for k, v in dense.items()}
+            with dgr.async_forward(True):
+                img = GaussianRasterizer(raster_settings=cam)(
+                    **dict(leaves, means2D=torch.zeros_like(leaves["means3D"], requires_grad=True)))[0]
+            torch.cuda.synchronize()
+            with pytest.raises(RuntimeError, match="gate timed out"):
+                (img * dl).sum().backward()
+            del img
+    finally:
+        _C.debug_async_fault(0, 0, clear=True)
+    gc.collect()
+    torch.cuda.synchronize()
+    _C.speculation_stats(reset=True)
+    _run(a, cam, "exact", dl)
+    _same(_run(dense, cam, "async", dl), _run(dense, cam, "exact", dl))

@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     L = _C.load_library()
-    assert L.gsr_abi_version() == _C.ABI_VERSION == 19
+    assert L.gsr_abi_version() == _C.ABI_VERSION == 20
     for P in (0, 1, 1000, 1_000_000):
         assert L.gsr_geom_bytes(P) % 256 == 0 and L.gsr_geom_bytes(P) >= 64 * P
     assert L.gsr_image_bytes(1920, 1080, 10) >= 1920 * 1080 * 8

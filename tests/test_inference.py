@@ -8,8 +8,9 @@ drop-in module on non-leaf activations.  Checked here on a 300k-Gaussian cloud:
 * radii bit-exact and colour / depth within 1e-4 (blend-threshold flips allowed at the headline's
   rate) against the oracle, for every camera;
 * no per-call workspace outlives the call: with no autograd graph the GEOM / IMAGE / BINNING buffers
-  (and any speculative BINNING) are released when the call returns, so the memory the caching
-  allocator holds for tensors grows by the outputs alone, and returns to where it was once they go.
+  (and any speculative BINNING) are released when the call returns, so the bytes requested from the
+  caching allocator (``requested_bytes``: exact sizes, not its block rounding) grow by the outputs
+  alone, and return to where they were once the outputs go.
 """
 import numpy as np
 import pytest
@@ -26,6 +27,10 @@ P = 300_000
 PIX_FLIP = 4e-5  # blend decisions on a threshold (test_gpu_parity.py ALLOW, the C2-size cases)
 
 
+def _requested(dev):
+    return torch.cuda.memory_stats(dev)["requested_bytes.all.current"]
+
+
 def _cloud(dev):
     return S.synthetic_cloud(P, 0.008, sh_degree=-1, seed=2, device=dev)
 
@@ -33,20 +38,21 @@ def _cloud(dev):
 def test_inference_rig_parity_and_workspace(cuda):
     params = _cloud(cuda)
     cams = S.inference_cameras(device=cuda)
-    cpu = {k: v.cpu() for k, v in params.items()}
-    a = {k: v.detach() for k, v in S.render_arguments(cpu).items() if k != "means2D"}
     torch.cuda.synchronize()
     for i, rs in enumerate(cams):
         with torch.no_grad():
             args = S.render_arguments(params)  # create_render_arguments, per render (train.py:544)
             torch.cuda.synchronize()
-            before = torch.cuda.memory_allocated(cuda)
+            before = _requested(cuda)
             img, radii, depth = GaussianRasterizer(raster_settings=rs)(**args)
             torch.cuda.synchronize()
-            after = torch.cuda.memory_allocated(cuda)
+            after = _requested(cuda)
         assert not img.requires_grad and img.grad_fn is None
+        # the oracle gets the very activations the GPU rendered (torch's GPU exp / sigmoid / normalize can
+        # differ from its CPU ones by an ulp, which can move a radius across an integer)
+        a = {k: v.detach().cpu() for k, v in args.items() if k != "means2D"}
         out_bytes = sum(t.untyped_storage().nbytes() for t in (img, radii, depth))
-        assert after - before <= out_bytes + 3 * 512, (
+        assert after - before == out_bytes, (
             f"camera {i}: {after - before} bytes held after the call, outputs are {out_bytes}")
         r = rs._replace(viewmatrix=rs.viewmatrix.cpu(), projmatrix=rs.projmatrix.cpu(), campos=rs.campos.cpu(),
                         bg=rs.bg.cpu())
@@ -59,4 +65,4 @@ def test_inference_rig_parity_and_workspace(cuda):
         _close("depth", _np(depth), st["depth"], atol_frac=1e-6, max_bad_frac=PIX_FLIP)
         del img, radii, depth, st
         torch.cuda.synchronize()
-        assert torch.cuda.memory_allocated(cuda) == before, f"camera {i}: memory not returned after the outputs went"
+        assert _requested(cuda) == before, f"camera {i}: memory not returned after the outputs went"

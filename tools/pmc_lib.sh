@@ -1,15 +1,24 @@
 #!/bin/bash
 # SQ counters of the render kernels for one library build (one pass of 8 SQ counters, short 1-stream bench).
-# usage (GPU box): bash tools/pmc_lib.sh OUTDIR NAME   (NAME = def or tools/ab/libgsr_NAME.so)
+# usage (GPU box): bash tools/pmc_lib.sh OUTDIR NAME [sq|lds]   (NAME = def or tools/ab/libgsr_NAME.so)
 set -u
-O=$1; v=$2
-if [ "$v" = def ]; then L=animating-gaussian-splats_amd/diff_gaussian_rasterization/libgsr.so; else L=tools/ab/libgsr_$v.so; fi
-R=$(pwd); mkdir -p "$O/pmc_$v"; OO=$(cd "$O/pmc_$v" && pwd)
-export GSR_LIB=$R/$L
+O=$1; v=$2; set_=${3:-sq}
+if [ "$set_" = lds ]; then
+  CTRS="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU"
+else
+  CTRS="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY"
+fi
+R=$(pwd); mkdir -p "$O/pmc_${v}_$set_"; OO=$(cd "$O/pmc_${v}_$set_" && pwd)
+B=$R/bench.py; EXTRA="--inference-steps 0"
+case "$v" in
+  def) export GSR_LIB=$R/animating-gaussian-splats_amd/diff_gaussian_rasterization/libgsr.so ;;
+  *tree) B=$R/tools/ab/$v/bench.py; EXTRA="" ;;
+  *) export GSR_LIB=$R/tools/ab/libgsr_$v.so ;;
+esac
 cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY \
-  --kernel-include-regex "render" --kernel-trace --output-format csv -d "$OO/sq" -- \
-  python3 "$R/bench.py" --no-cpu-baseline --streams 1 --steps 6 --warmup 2 --probe-steps 1 --call-site-steps 0 --train-steps 0 --c2-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0 > "$OO/log" 2>&1 || { echo "pmc failed"; tail -5 "$OO/log"; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc $CTRS \
+  --kernel-include-regex "render|sort" --kernel-trace --output-format csv -d "$OO/sq" -- \
+  python3 "$B" --no-cpu-baseline --streams 1 --steps 6 --warmup 2 --probe-steps 1 --call-site-steps 0 --train-steps 0 --c2-steps 0 --unchanged-steps 0 $EXTRA --loss-steps 0 --densify-steps 0 --io-timesteps 0 > "$OO/log" 2>&1 || { echo "pmc failed"; tail -5 "$OO/log"; exit 1; }
 cd "$R"
 python3 - "$OO" "$v" <<'PY'
 import csv, glob, sys, collections
