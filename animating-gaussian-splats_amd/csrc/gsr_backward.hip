@@ -153,8 +153,10 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
     d[2] = F3{r6, r7, r8};
 }
 
-// the register budget of 5 waves per SIMD (96 VGPRs; 6 waves spilled and ran slower)
-#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(5, 8)))
+// the register budget: 6 waves per SIMD (80 VGPRs, no spills since the record inputs wait in LDS;
+// 3 % faster alone than 5 waves, profiles/r05_bwd_waves_ab.txt); the exact-threshold variant keeps 5
+// (96 VGPRs: its near-threshold call site needs the registers)
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 5 : 6, 8)))
 constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
 
 // ---- the pair reduction ---------------------------------------------------------------------------
@@ -186,18 +188,16 @@ __device__ inline void row_halves3(float &X, float &Y, float &Z) {
         "v_add_f32_dpp %2, %2, %2 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
         : "+v"(X), "+v"(Y), "+v"(Z));
 }
-struct RowW { float mx, cx, m0, m2; };  // per-lane weight coefficients of its row (see pair_sums)
-__device__ inline RowW row_weights(int row) {
-    return RowW{row == 0 ? 1.f : 0.f, row == 0 ? 0.f : 1.f, row == 0 ? 1.f : 0.f, row == 2 ? 1.f : 0.f};
-}
+struct RowW { bool r0, r2; };  // the lane's row of the folded column sums is row 0 / row 2 (lane masks)
+__device__ inline RowW row_weights(int row) { return RowW{row == 0, row == 2}; }
 struct PairSums { float X, Y, Z; };
 __device__ inline PairSums pair_sums(float S0, float S1, float S4, float cs0, float cs1, float cs2, float dx,
                                      const RowW &w) {
     const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(cs1, cs2);
     const float rA = fold16(pA, pB);   // column sums, rows [S0, S4, S1, cs0]
     const float rC = fold16(0.f, pC);  // rows [0, cs1, 0, cs2]
-    const float wx = fmaf(w.mx, dx, w.cx);       // row 0: dx, else 1
-    const float wy = dx * fmaf(w.m0, dx, w.m2);  // row 0: dx^2, row 2: dx, else 0
+    const float wx = w.r0 ? dx : 1.f;                           // row 0: dx, else 1
+    const float wy = w.r0 ? dx * dx : (w.r2 ? dx : 0.f);        // row 0: dx^2, row 2: dx, else 0
     PairSums r{rA * wx, fmaf(rA, wy, rC), rA};
     row_halves3(r.X, r.Y, r.Z);
     return r;
@@ -308,12 +308,17 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     // (one address VGPR per pair, the rest immediate offsets).
     constexpr int kStage = 64 * kBwdWaves;
     __shared__ float4 s_stage[3 * kStage];
+    __shared__ float2 s_tail_all[kStage];  // per staged entry: (exact conic c, emission index) for the record
     __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
     if (spec_ok && *spec_ok == 0u) return;  // speculative render half whose forward was redone: redone too
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t item = blockIdx.x * kBwdWaves + wv;
     if (item >= items[0].x) return;  // the launch covers the item bound
-    float4 *s_a = s_stage + 64 * wv;  // (x, y, A2, B2); + kStage: (C2, opacity, -, -); + 2 kStage: colour + mask
+    // per staged entry: (x, y, A2, B2); + kStage: (C2, opacity, exact conic a, b); + 2 kStage: colour +
+    // quarter mask; s_tail: (exact conic c, emission index) -- the record's inputs wait in LDS, not in
+    // registers, while the batch is walked
+    float4 *s_a = s_stage + 64 * wv;
+    float2 *s_tail = s_tail_all + 64 * wv;
     float *s_out = s_out_all + 64 * kPartial * wv;
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -400,11 +405,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     for (int end = s1; end > s0; end -= 64) {
         const int start = end - 64 > s0 ? end - 64 : s0;
         const int cnt = end - start;
-        const uint32_t em = em_n;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, cj = a;
         if (lane < cnt) {
             const float4 *r = rec + (size_t)kRecF4 * g_n;
             a = r[0]; b = r[1]; c = r[2]; cj = r[3];  // cj: exact conic (a, b, c) of the staged Gaussian
+            s_tail[lane] = make_float2(cj.z, __uint_as_float(em_n));
         }
         if (end - 64 > s0) fetch(end - 64);
 #pragma unroll
@@ -418,7 +423,7 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
         if (lane < cnt) {
             const uint32_t p = (uint32_t)(start + lane);
             s_a[lane] = a;
-            s_a[kStage + lane] = b;
+            s_a[kStage + lane] = make_float4(b.x, b.y, cj.x, cj.y);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (p < qmax[k] &&
@@ -438,14 +443,18 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
             float sm[kPartial];
 #pragma unroll
             for (int q = 0; q < kPartial; ++q) sm[q] = s2[q];
+            const float4 bj = s_a[kStage + lane];  // (C2, opacity, exact conic a, b)
+            const float2 tl = s_tail[lane];         // (exact conic c, emission index)
+            const float o = bj.y;
+            const uint32_t em = __float_as_uint(tl.y);
             // sums of sG = o G dL/dalpha: the opacity is already in; dL/dopacity = sum G dL/dalpha
             rec_store(part, em,
-                      (-cj.x * sm[0] - cj.y * sm[2]) * half_w,  // dL/dmeans2D.x (NDC)
-                      (-cj.y * sm[0] - cj.z * sm[2]) * half_h,  // dL/dmeans2D.y (NDC)
+                      (-bj.z * sm[0] - bj.w * sm[2]) * half_w,  // dL/dmeans2D.x (NDC)
+                      (-bj.w * sm[0] - tl.x * sm[2]) * half_h,  // dL/dmeans2D.y (NDC)
                       -0.5f * sm[4],                            // dL/dconic.a
                       -0.5f * sm[6],                            // dL/dconic.b (b/2 convention)
                       -0.5f * sm[1],                            // dL/dconic.c
-                      sm[8] != 0.f ? sm[8] / b.y : 0.f,         // dL/dopacity
+                      sm[8] != 0.f ? sm[8] / o : 0.f,           // dL/dopacity
                       sm[3], sm[5], sm[7]);                     // dL/dcolour
         }
     }
