@@ -1094,6 +1094,7 @@ def main():
             traffic_2x = int(pm["hbm_bytes_per_launch_corrected"])
             traffic = calibrated_traffic(pm, dom, cfg.P, K, N, T)
     valu = None
+    solo_ms = solo[dom][0] / solo[dom][1] if solo and solo[dom][1] else None
     if os.path.exists(SQ_SUMMARY) and args.config == "C3":
         q = json.load(open(SQ_SUMMARY)).get("k_" + dom)
         if q and "SQ_INSTS_VALU" in q:
@@ -1101,7 +1102,7 @@ def main():
             # vs one per 2 cycles on every SIMD (the v_fma_f32 rate; transcendentals, DPP and permlane
             # ops occupy the pipe 2-4x longer: tools/valu_rate_probe.hip), so issue_frac is a floor
             # on the VALU pipe's busy share
-            rate = q["SQ_INSTS_VALU"] / (avg_ms * 1e-3) / 1e9
+            rate = q["SQ_INSTS_VALU"] / ((solo_ms or avg_ms) * 1e-3) / 1e9
             valu = {"insts_per_launch": int(q["SQ_INSTS_VALU"]),
                     "trans_insts_per_launch": int(q.get("SQ_INSTS_VALU_TRANS_F32", 0)),
                     "achieved_Ginst_s": round(rate, 1), "peak_Ginst_s": VALU_PEAK_GINST,
@@ -1111,11 +1112,12 @@ def main():
                 pk = 1024 * q["clock_ghz"] / 2  # Ginst/s at that clock
                 valu["profile_clock_ghz"] = round(q["clock_ghz"], 3)
                 valu["issue_frac_at_profile_clock"] = round(rate / pk, 4)
-    solo_ms = solo[dom][0] / solo[dom][1] if solo and solo[dom][1] else None
-    if valu is not None and solo_ms:
-        valu["solo_issue_frac"] = round(valu["insts_per_launch"] / (solo_ms * 1e-3) / 1e9 / VALU_PEAK_GINST, 4)
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, SH)
-    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+    # the roofline uses the kernel's own duration: the solo probe (one stream, nothing else on the chip)
+    # when there is one; the in-step event interval (which overlaps the other streams' kernels) is
+    # reported beside it, labelled as such
+    kernel_ms = solo_ms if solo_ms else avg_ms
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     # value: the median step (median of >= 20 reps) -- per-step device intervals
     # between the step-end events on the main stream; the mean over the timed region beside it
@@ -1182,10 +1184,13 @@ def main():
                          "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if traffic else None,
                          "traffic_2x_fetch": traffic_2x,
                          "traffic_calibration": "profiles/r01_fetch_calib.txt" if traffic else None,
-                         "avg_kernel_ms": round(avg_ms, 5), "algorithmic_bytes": int(bytes_launch),
-                         # the same kernel alone (solo probe: one stream, no concurrent kernels)
-                         "solo_avg_kernel_ms": round(solo_ms, 5) if solo_ms else None,
-                         "solo_frac": round(bytes_launch / (solo_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5) if solo_ms else None,
+                         "avg_kernel_ms": round(kernel_ms, 5), "algorithmic_bytes": int(bytes_launch),
+                         "duration_basis": ("solo probe: the kernel alone on one stream, HIP events on its launch "
+                                            "stream inside libgsr" if solo_ms else "in-step event interval"),
+                         # the interval between HIP events around the kernel inside the pipelined step: it
+                         # overlaps the other streams' kernels, so it is not the kernel's own time
+                         "in_step_interval_ms": round(avg_ms, 5),
+                         "in_step_frac": round(bytes_launch / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
                          "algorithmic_bytes_formula": {"render_bwd": "K*40 + N*20 + T*16",
                                                        "render_fwd": "K*44 + N*24 + T*16",
                                                        "gauss_bwd": "P*(84+F) + P*(56+F)"}.get(dom),

@@ -8,7 +8,7 @@
 # outputs: gpurun_out/prof_<tag>/{trace,fetch,write,sq1,sq2}/ raw CSV, trace_summary.txt, hbm_pmc.json, sq_pmc.json
 set -u
 tag=${1:-r01}; shift || true
-BENCH_LEGS="--call-site-steps 0 --train-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0 --unchanged-steps 0 --c2-steps 0 --steps 20 --warmup 5"
+BENCH_LEGS="--call-site-steps 0 --inference-steps 0 --train-steps 0 --loss-steps 0 --densify-steps 0 --io-timesteps 0 --unchanged-steps 0 --c2-steps 0 --steps 20 --warmup 5"
 R=$(pwd)
 O=$R/gpurun_out/prof_$tag
 mkdir -p "$O"
