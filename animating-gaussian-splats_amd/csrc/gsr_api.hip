@@ -198,10 +198,11 @@ int check_common(const gsr_camera *cam, const gsr_gaussians *g, bool need_opacit
     return GSR_OK;
 }
 
-// exact-threshold mode (gsr_set_exact_thresholds; GSR_EXACT_THRESHOLDS=1 at load)
+// exact-threshold mode (gsr_set_exact_thresholds): on by default, GSR_EXACT_THRESHOLDS=0 at load turns
+// it off
 std::atomic<int> g_exact{[] {
     const char *e = getenv("GSR_EXACT_THRESHOLDS");
-    return (e && e[0] == '1') ? 1 : 0;
+    return (e && e[0] == '0') ? 0 : 1;
 }()};
 
 void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
@@ -243,6 +244,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.meta = (uint32_t *)(base + L.meta); a.chunk_off = (uint32_t *)(base + L.chunk_off);
     a.items_ws = (uint32_t *)(base + L.items_ws);
     a.scan_ws = (uint32_t *)(base + L.scan_ws); a.tile_rank = (uint32_t *)(base + L.tile_rank);
+    a.tile_flag = (uint32_t *)(base + L.tile_flag); a.near_rec = (float4 *)(base + L.near_rec);
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K, a.P);
@@ -286,11 +288,11 @@ int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const GeomLayout g(P);
     const ImageLayout im(W, H, P);
     const BinningLayout b(K, P);
-    const size_t v[14] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
+    const size_t v[15] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
                           im.ranges, im.pix_end, im.n_contrib, im.tile_maxc,
-                          b.pairs, b.point_list, b.slot_emit, im.seg_off, b.seg_state};
+                          b.pairs, b.point_list, b.slot_emit, im.seg_off, b.seg_state, im.tile_flag};
     int n = 0;
-    for (; n < 14 && n < max_out; ++n) out[n] = v[n];
+    for (; n < 15 && n < max_out; ++n) out[n] = v[n];
     return n;
 }
 
@@ -539,7 +541,7 @@ int async_redo(AsyncFwd &f, hipStream_t H) {
     HIP_TRY(launch_tile_sort(a, n_mid, n_vlong, max_n, (uint4 *)((char *)bin + bin_bytes + item_bytes), H));
     HIP_TRY(launch_render_fwd(a, H));
     if (f.prep)
-        HIP_TRY(launch_bwd_items_raw((int)K, f.T, a.P, a.ranges, a.tile_maxc, (uint2 *)((char *)bin + bin_bytes), a.items_ws, H));
+        HIP_TRY(launch_bwd_items_raw((int)K, f.T, a.P, a.ranges, a.tile_maxc, a.tile_flag, (uint2 *)((char *)bin + bin_bytes), a.items_ws, H));
     HIP_TRY(hipStreamSynchronize(H));
     f.bin = bin;
     f.layout = (int)K;
@@ -727,7 +729,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
         if (g->prepare_backward) {
             uint2 *items = (uint2 *)(spec_bin + BinningLayout((int)cap, a.P).total);
             Phase ph(s, "bwd_items");
-            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, s, sa.spec_ok));
+            HIP_TRY(launch_bwd_items_raw((int)cap, T, a.P, a.ranges, a.tile_maxc, a.tile_flag, items, a.items_ws, s, sa.spec_ok));
         }
     }
     if (af) {  // asynchronous: gate the stream on the verdict and return
@@ -797,7 +799,7 @@ int forward_impl(const gsr_camera *cam, const gsr_gaussians *g, gsr_alloc_fn all
     if (g->prepare_backward) {  // the backward's item list, built here, off its critical path
         uint2 *items = (uint2 *)(bin + bin_bytes);
         Phase ph(s, "bwd_items");
-        HIP_TRY(launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, items, a.items_ws, s));
+        HIP_TRY(launch_bwd_items_raw((int)K, T, a.P, a.ranges, a.tile_maxc, a.tile_flag, items, a.items_ws, s));
     }
     info->binning_layout = (int)K;
     spec_record(key, K, n_vlong > 0, cap ? -1 : 0, n_mid);
@@ -991,7 +993,8 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     a.radii = radii;
     a.rec = f.rec; a.rect = f.rect; a.goff = f.goff; a.clampm = f.clampm;
     a.ranges = f.ranges; a.pix_end = f.pix_end; a.n_contrib = f.n_contrib; a.tile_maxc = f.tile_maxc;
-    a.seg_off = f.seg_off; a.meta = f.meta; a.items_ws = f.items_ws; a.exact = f.exact;
+    a.tile_flag = f.tile_flag; a.near_rec = f.near_rec;
+    a.seg_off = f.seg_off; a.meta = f.meta; a.items_ws = f.items_ws;
     a.point_list = f.point_list; a.slot_emit = f.slot_emit; a.seg_state = f.seg_state;
     a.dL_dcolor = dL_dcolor;
     a.spec_ok = spec ? f.meta + 1 : nullptr;

@@ -53,6 +53,7 @@ __device__ inline void for_tile_items(uint32_t n, uint4 mq, int ks, const ItemBu
 
 __global__ __launch_bounds__(kItemsBlock) void k_items_count(int T, const uint2 *__restrict__ ranges,
                                                              const uint32_t *__restrict__ tile_maxc,
+                                                             const uint32_t *__restrict__ tile_flag,
                                                              uint2 *__restrict__ items, uint32_t *__restrict__ ws,
                                                              const uint32_t *__restrict__ spec_ok, int ks) {
     __shared__ uint32_t s_hist[kOrderBuckets];
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(kItemsBlock) void k_items_count(int T, const uint2 
     __syncthreads();
     const ItemBucket bk(ks);
     const int t = blockIdx.x * kItemsBlock + (int)threadIdx.x;
-    if (t < T) {
+    if (t < T && tile_flag[t] <= kNearCap) {  // (near-record overflow tiles' items are listed after these)
         const uint2 rg = ranges[t];
         const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[t];
         for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t, uint32_t b) { atomicAdd(&s_hist[b], 1u); });
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(kItemsBlock) void k_items_count(int T, const uint2 
 
 __global__ __launch_bounds__(kItemsBlock) void k_items_emit(int T, const uint2 *__restrict__ ranges,
                                                             const uint32_t *__restrict__ tile_maxc,
+                                                            const uint32_t *__restrict__ tile_flag,
                                                             uint2 *__restrict__ items, uint32_t *__restrict__ ws,
                                                             const uint32_t *__restrict__ spec_ok, int ks) {
     __shared__ uint32_t s_cur[kOrderBuckets];
@@ -116,14 +118,24 @@ __global__ __launch_bounds__(kItemsBlock) void k_items_emit(int T, const uint2 *
     const int t = blockIdx.x * kItemsBlock + (int)threadIdx.x;
     const uint2 rg = t < T ? ranges[t] : make_uint2(0, 0);
     const uint4 mq = t < T ? reinterpret_cast<const uint4 *>(tile_maxc)[t] : make_uint4(0, 0, 0, 0);
-    for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t, uint32_t b) { atomicAdd(&s_cur[b], 1u); });
+    const bool ex = t < T && tile_flag[t] > kNearCap;
+    // a tile with more near-threshold records than kNearCap: its items go after the others' ([0].x of
+    // them), unordered, counted in [0].y (zeroed by k_items_count), for k_render_bwd<true>
+    if (ex) {
+        const uint32_t base = 1u + items[0].x;
+        for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t code, uint32_t) {
+            items[base + atomicAdd(&items[0].y, 1u)] = make_uint2((uint32_t)t, code);
+        });
+    }
+    const uint32_t n = ex ? 0u : rg.y - rg.x;
+    for_tile_items(n, mq, ks, bk, [&](uint32_t, uint32_t b) { atomicAdd(&s_cur[b], 1u); });
     lds_barrier();  // (no-return LDS atomics)
     for (int b = threadIdx.x; b < kOrderBuckets; b += blockDim.x) {  // this block's run in each bucket
         const uint32_t h = s_cur[b];
         if (h) s_cur[b] = atomicAdd(&ws[kOrderBuckets + b], h);
     }
     lds_barrier();
-    for_tile_items(rg.y - rg.x, mq, ks, bk, [&](uint32_t code, uint32_t b) {
+    for_tile_items(n, mq, ks, bk, [&](uint32_t code, uint32_t b) {
         items[1 + atomicAdd(&s_cur[b], 1u)] = make_uint2((uint32_t)t, code);
     });
 }
@@ -156,8 +168,9 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
 // the register budget: 6 waves per SIMD (80 VGPRs, no spills since the record inputs wait in LDS;
 // 3 % faster alone than 5 waves, profiles/r05_bwd_waves_ab.txt); the exact-threshold variant keeps 5
 // (96 VGPRs: its near-threshold call site needs the registers)
-#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 5 : 6, 8)))
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 4 : 6, 8)))
 constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
+constexpr int kExactBwdBlocks = 256;  // grid of the exact-threshold tiles' k_render_bwd
 
 // ---- the pair reduction ---------------------------------------------------------------------------
 // Every lane holds, for its 4 pixels of one column, S0 = sum sG, S1 = sum sG dy, S4 = sum sG dy^2 and
@@ -214,20 +227,39 @@ struct LaneSums { float S0, S1, S4, c0, c1, c2; };
 // that does not take the pair gets alpha = 0, which makes every update an identity (r = 1, AR
 // unchanged, zero sums).  The blend weight is pair_power + 2^x, the forward's exact operation
 // sequence, hence bitwise-identical decisions.
-template <bool CLAMP, bool EXACT>
+// NEAR (exact-threshold mode, a tile whose forward re-evaluated near-threshold weights): kNearLook --
+// a weight in the near window takes the forward's re-evaluated (power, G, alpha) from the tile's near
+// records (key: list position << 8 | pixel k of the lane = lane + 64 k); kNearEval -- re-evaluated here
+// as the forward did (a tile with more records than kNearCap).  Either way the forward's decisions.
+constexpr int kNearNone = 0, kNearLook = 1, kNearEval = 2;
+struct NearRecs { const float4 *r; uint32_t n; int start; };  // the tile's records, the batch's list start
+template <bool CLAMP, int NEAR>
 __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &any, const PairX &x, float4 a,
-                                             float C2, float o, float4 c, int j, float pfx,
-                                             const float4 *__restrict__ rec, const uint32_t *__restrict__ pl) {
+                                             float C2, float o, float4 c, int j, int k, float pfx,
+                                             const float4 *__restrict__ rec, const uint32_t *__restrict__ pl,
+                                             const NearRecs &nrs) {
     const float dy = a.y - ps.fy;  // same operation as the forward's
     float p2 = pair_power(x, C2, dy);
     float G = __builtin_amdgcn_exp2f(p2);
     float alpha = CLAMP ? fminf(0.99f, o * G) : o * G;
     const bool live = j < ps.lrel;  // the entry lies before this pixel's last contributor
-    if constexpr (EXACT) {  // the forward's near-threshold re-evaluation: the same decisions
+    if constexpr (NEAR == kNearEval) {  // the forward's near-threshold re-evaluation: the same decisions
         const bool nr = live && near_threshold(alpha);
-        if (__builtin_amdgcn_ballot_w64(nr) && nr) {
+        if (nr) {  // (an exec-masked region, skipped when no lane has one)
             const ExactBlend e = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * pl[j] + 3], o, pfx, ps.fy);
             p2 = e.power; G = e.G; alpha = e.alpha;
+        }
+    } else if constexpr (NEAR == kNearLook) {
+        const bool nr = live && p2 <= 0.0f && near_threshold(alpha);
+        if (nr) {  // (an exec-masked region, skipped when no lane has one)
+            const uint32_t key = ((uint32_t)(nrs.start + j) << 8) | (uint32_t)((threadIdx.x & 63) + 64 * k);
+            for (uint32_t i = 0; i < nrs.n; ++i) {  // (uniform loads)
+                const float4 r = nrs.r[i];
+                const bool hit = __float_as_uint(r.x) == key;
+                p2 = hit ? r.y : p2;
+                G = hit ? r.z : G;
+                alpha = hit ? r.w : alpha;
+            }
         }
     }
     const bool ok = live && p2 <= 0.0f && alpha >= 1.0f / 255.0f;
@@ -257,10 +289,10 @@ __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &an
 // The walk of one batch: every staged pair j (descending) over the quarters of its mask; each pair's
 // sums are reduced and added into its s_out slot when any pixel of the wave took it.  CLAMP: some
 // staged pair's opacity exceeds 0.99 (batch-uniform, so the pair loop itself has no variant branch).
-template <bool CLAMP, bool EXACT>
+template <bool CLAMP, int NEAR>
 __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const float4 *s_a, float pfx,
                                            const RowW &rw, float *o_row, const float4 *__restrict__ rec,
-                                           const uint32_t *__restrict__ pl) {
+                                           const uint32_t *__restrict__ pl, const NearRecs &nrs) {
     constexpr int kStage = 64 * kBwdWaves;
     while (m) {
         const int j = 63 - __builtin_clzll(m);
@@ -275,7 +307,7 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
-            eval_quarter<CLAMP, EXACT>(ps[k], s, any, x, a, b.x, b.y, c, j, pfx, rec, pl);
+            eval_quarter<CLAMP, NEAR>(ps[k], s, any, x, a, b.x, b.y, c, j, k, pfx, rec, pl, nrs);
         }
         // the skip pays although only ~3 % of the walked pairs have no taker (tools/contrib_stats.py):
         // always reducing measured 0.325 vs 0.316 ms alone (profiles/r05_bwd_micro_ab.txt)
@@ -291,41 +323,24 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
     }
 }
 
+// One (tile, segment) item of k_render_bwd on one wave, with the wave's LDS slices: per staged entry
+// (x, y, A2, B2); + kStage: (C2, opacity, exact conic a, b); + 2 kStage: colour + quarter mask; s_tail:
+// (exact conic c, emission index) -- the record's inputs wait in LDS, not in registers, while the
+// batch is walked.
 template <bool EXACT>
-__global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
-    int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
+__device__ __forceinline__ void bwd_item(
+    uint2 it, uint32_t item, int W, int H, int gx, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
     const float4 *__restrict__ rec, const float *__restrict__ bg, const float4 *__restrict__ pix_end,
     const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
-    float4 *__restrict__ part, int ks, const uint32_t *__restrict__ spec_ok) {
-    // Each wave of the workgroup takes its own item and its own LDS slice; the waves never
-    // synchronise with each other.  Items are in descending cost order, so the kBwdWaves items of
-    // one workgroup cost about the same: grouping them keeps the launch's workgroups coarse, which
-    // leaves the CUs' free slots to the forward kernels of the other streams in a pipelined step
-    // (one-wave workgroups take every slot a finishing wave frees and starve their large-LDS
-    // workgroups).
-    // Staging: one array, so the three record parts of entry j are at fixed offsets from one address
-    // (one address VGPR per pair, the rest immediate offsets).
+    float4 *__restrict__ part, int ks, const uint32_t *__restrict__ tile_flag,
+    const float4 *__restrict__ near_rec, float4 *s_a, float2 *s_tail, float *s_out) {
     constexpr int kStage = 64 * kBwdWaves;
-    __shared__ float4 s_stage[3 * kStage];
-    __shared__ float2 s_tail_all[kStage];  // per staged entry: (exact conic c, emission index) for the record
-    __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
-    if (spec_ok && *spec_ok == 0u) return;  // speculative render half whose forward was redone: redone too
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t item = blockIdx.x * kBwdWaves + wv;
-    if (item >= items[0].x) return;  // the launch covers the item bound
-    // per staged entry: (x, y, A2, B2); + kStage: (C2, opacity, exact conic a, b); + 2 kStage: colour +
-    // quarter mask; s_tail: (exact conic c, emission index) -- the record's inputs wait in LDS, not in
-    // registers, while the batch is walked
-    float4 *s_a = s_stage + 64 * wv;
-    float2 *s_tail = s_tail_all + 64 * wv;
-    float *s_out = s_out_all + 64 * kPartial * wv;
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const uint2 it = items[1 + item];
     const int tile = (int)it.x;
     const uint32_t seg = it.y;
     const uint2 rg = ranges[tile];
@@ -393,6 +408,8 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     }
     const RowW rw = row_weights(lane >> 4);
     float *o_row = s_out + (lane >> 4);  // this lane's row slot of every pair's sums
+    // the tile's near records (exact-threshold mode; none when its forward re-evaluated no weight)
+    NearRecs nrs{near_rec + (size_t)kNearCap * tile, EXACT ? 0u : tile_flag[tile], 0};
     // the point list entry of each batch's slot is loaded one batch ahead (the render record gathers
     // depend on it); the records themselves are gathered at the batch start
     uint32_t g_n = 0, em_n = 0;
@@ -437,8 +454,20 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
         uint64_t m = __ballot(qmask != 0);
         wave_lds_sync();
         const uint32_t *pl = point_list + rg.x + start;
-        if (__builtin_amdgcn_ballot_w64(qmask & 16u)) walk_batch<true, EXACT>(ps, m, s_a, pfx, rw, o_row, rec, pl);
-        else walk_batch<false, EXACT>(ps, m, s_a, pfx, rw, o_row, rec, pl);
+        const bool clamp = __builtin_amdgcn_ballot_w64(qmask & 16u) != 0;
+        if constexpr (EXACT) {
+            if (clamp) walk_batch<true, kNearEval>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+            else walk_batch<false, kNearEval>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+        } else {
+            nrs.start = start;
+            if (nrs.n) {  // (wave-uniform: the tile's forward re-evaluated near-threshold weights)
+                if (clamp) walk_batch<true, kNearLook>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+                else walk_batch<false, kNearLook>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+            } else {
+                if (clamp) walk_batch<true, kNearNone>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+                else walk_batch<false, kNearNone>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+            }
+        }
         wave_lds_sync();
         if (lane < cnt) {
             const float *s2 = s_out + lane * kPartial;
@@ -463,6 +492,47 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
 #ifdef GSR_TRACE
     trace_wave(g_trace_bwd, item, t_start, 0);
 #endif
+}
+
+
+template <bool EXACT>
+__global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
+    int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
+    const uint32_t *__restrict__ point_list,
+    const float4 *__restrict__ rec, const float *__restrict__ bg, const float4 *__restrict__ pix_end,
+    const uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ tile_maxc,
+    const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
+    const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
+    float4 *__restrict__ part, int ks, const uint32_t *__restrict__ spec_ok,
+    const uint32_t *__restrict__ tile_flag, const float4 *__restrict__ near_rec) {
+    // Each wave of the workgroup takes its own item and its own LDS slice; the waves never
+    // synchronise with each other.  Items are in descending cost order, so the kBwdWaves items of
+    // one workgroup cost about the same: grouping them keeps the launch's workgroups coarse, which
+    // leaves the CUs' free slots to the forward kernels of the other streams in a pipelined step
+    // (one-wave workgroups take every slot a finishing wave frees and starve their large-LDS
+    // workgroups).
+    // Staging: one array, so the three record parts of entry j are at fixed offsets from one address
+    // (one address VGPR per pair, the rest immediate offsets).
+    constexpr int kStage = 64 * kBwdWaves;
+    __shared__ float4 s_stage[3 * kStage];
+    __shared__ float2 s_tail_all[kStage];  // per staged entry: (exact conic c, emission index) for the record
+    __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
+    if (spec_ok && *spec_ok == 0u) return;  // speculative render half whose forward was redone: redone too
+    // (the wave index as a scalar: the item, its tile and everything derived from them live in SGPRs)
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4 *s_a = s_stage + 64 * wv;
+    float2 *s_tail = s_tail_all + 64 * wv;
+    float *s_out = s_out_all + 64 * kPartial * wv;
+    const uint2 hd = items[0];  // (items, items of the tiles with more than kNearCap near records after them)
+    if constexpr (EXACT) {
+        // the tiles with more near-threshold weights than kNearCap (rare): every wave loops over them
+        for (uint32_t i = blockIdx.x * kBwdWaves + wv; i < hd.y; i += gridDim.x * kBwdWaves)
+            bwd_item<true>(items[1 + hd.x + i], hd.x + i, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_tail, s_out);
+    } else {
+        const uint32_t item = blockIdx.x * kBwdWaves + wv;
+        if (item >= hd.x) return;  // the launch covers the item bound
+        bwd_item<false>(items[1 + item], item, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_tail, s_out);
+    }
 }
 
 // Gradient output write: plain store, or (accumulate bit set, gsr_grads.accumulate) add into the
@@ -1180,26 +1250,32 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 
 
 // ==========================================================================================
-hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
-                                uint32_t *ws, hipStream_t s, const uint32_t *spec_ok) {
+hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc,
+                                const uint32_t *tile_flag, uint2 *items, uint32_t *ws, hipStream_t s,
+                                const uint32_t *spec_ok) {
     if (K == 0) return hipSuccess;
     const int nb = div_up(T, kItemsBlock);
-    k_items_count<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
-    k_items_emit<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, items, ws, spec_ok, seg_log2(P));
+    k_items_count<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, tile_flag, items, ws, spec_ok, seg_log2(P));
+    k_items_emit<<<nb, kItemsBlock, 0, s>>>(T, ranges, tile_maxc, tile_flag, items, ws, spec_ok, seg_log2(P));
     return hipGetLastError();
 }
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s) {
-    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.P, a.ranges, a.tile_maxc, a.items, a.items_ws, s);
+    return launch_bwd_items_raw(a.K, a.gx * a.gy, a.P, a.ranges, a.tile_maxc, a.tile_flag, a.items, a.items_ws, s);
 }
 
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     if (a.K == 0) return hipSuccess;
     // one wave per item, kBwdWaves per workgroup; the launch covers the item bound, waves without an
-    // item exit at once
-    auto k = a.exact ? k_render_bwd<true> : k_render_bwd<false>;
-    k<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg,
-                                                                     a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off, a.seg_state,
-                                                                     a.slot_emit, a.dL_dcolor, a.part, seg_log2(a.P), a.spec_ok);
+    // item exit at once.  Then the items of the tiles whose near-threshold records overflowed (tile_flag
+    // > kNearCap; none when the exact-threshold mode is off) on a small grid that loops over their
+    // device-side count.
+    const int ks = seg_log2(a.P);
+    k_render_bwd<false><<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(
+        a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg, a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off,
+        a.seg_state, a.slot_emit, a.dL_dcolor, a.part, ks, a.spec_ok, a.tile_flag, a.near_rec);
+    k_render_bwd<true><<<std::min(div_up((int)a.max_items, kBwdWaves), kExactBwdBlocks), 64 * kBwdWaves, 0, s>>>(
+        a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg, a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off,
+        a.seg_state, a.slot_emit, a.dL_dcolor, a.part, ks, a.spec_ok, a.tile_flag, a.near_rec);
     return hipGetLastError();
 }
 

@@ -153,9 +153,12 @@ __host__ __device__ inline uint32_t lpt_bucket(uint32_t c) {
 //   pix_end: per pixel (C0, C1, C2, T) at the end of the blend (accumulated colour without the
 //            background, final transmittance);  seg_off: per tile, exclusive prefix of its interior
 //            segment boundaries (seg_bounds) -> index of its first saved boundary state.
+// near records per tile (IMAGE near_rec): the forward's re-evaluated (pixel, entry) weights, which the
+// backward looks up instead of re-evaluating; a tile with more re-evaluates in the backward as well
+constexpr uint32_t kNearCap = 16;
 struct ImageLayout {
     size_t ranges, pix_end, n_contrib, tile_maxc, tile_order_f, seg_off, sort_lists,
-        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, scan_ws, tile_rank, chunk_off, total;
+        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, scan_ws, tile_rank, tile_flag, near_rec, chunk_off, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -176,6 +179,8 @@ struct ImageLayout {
         items_ws = o;    o = align256(o + sizeof(uint32_t) * kItemsWsWords);
         scan_ws = o;     o = align256(o + sizeof(uint32_t) * kScanWsWords);
         tile_rank = o;   o = align256(o + sizeof(uint32_t) * T);           // rank inside its LPT bucket
+        tile_flag = o;   o = align256(o + sizeof(uint32_t) * T);           // near-threshold re-evaluations
+        near_rec = o;    o = align256(o + sizeof(float4) * kNearCap * T);  // and their records
         // (chunk, tile) counts, then each chunk's slab offset inside the tile's range (LDS binning)
         chunk_off = o;   o = align256(o + (T <= kMaxLdsTiles ? sizeof(uint32_t) * (size_t)NB * T : 0));
         total = o;

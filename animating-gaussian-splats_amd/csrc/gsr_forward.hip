@@ -869,7 +869,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
     float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok,
-    int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err, uint64_t gate_timeout) {
+    int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err, uint64_t gate_timeout,
+    uint32_t *__restrict__ tile_flag, float4 *__restrict__ near_rec) {
     __shared__ uint64_t s_key[sort_slots(kFwdSortCap)];
     __shared__ union {
         uint32_t val[sort_slots(kFwdSortCap)];  // sort payload (emission index), until written out
@@ -882,6 +883,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         } st;
     } s_u;
     __shared__ uint32_t s_live;     // quarters (bits) with an unsaturated pixel
+    __shared__ uint32_t s_near;     // (EXACT) near-threshold weights re-evaluated in this tile
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -893,6 +895,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     const uint2 rg = ranges[tile];
     const int n = (int)(rg.y - rg.x);
     const bool sorted_here = n <= kFwdSortCap;
+    if (threadIdx.x == 0) s_near = 0;  // (ordered before its atomics by the barrier ahead of the blend)
     if (n > 0 && sorted_here) {
         if (n <= 256) block_sort_tile<1, 4>(n, rg.x, pairs, s_key, s_u.val);
         else if (n <= 512) block_sort_tile<2, 4>(n, rg.x, pairs, s_key, s_u.val);
@@ -922,9 +925,13 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     // The pixel's alpha threshold: 1/255 while it blends, 2 (above any alpha <= 0.99) once it is done
     // (outside the image, or saturated): a finished pixel fails the same compare instead of carrying
     // a done flag through the loop as a lane mask (its mask logic cost ~7 scalar instructions per
-    // blended entry).  The decisions are those of !done && blend_ok(e).
+    // blended entry).  The decisions are those of !done && blend_ok(e).  EXACT: the live threshold is
+    // the lower end of the near window, kNearLo; a weight in [kNearLo, kNearHi) is re-evaluated (and
+    // compared with 1/255), any other weight is on the same side of kNearLo as of 1/255.
     constexpr float kThrDone = 2.0f;
-    float thr = inside ? 1.0f / 255.0f : kThrDone;
+    constexpr float kThrLive = EXACT ? kNearLo : 1.0f / 255.0f;
+    float thr = inside ? kThrLive : kThrDone;
+    const uint32_t pix_key = (uint32_t)(16 * ly + lx);  // near record key: (list position << 8) | pixel
     if (threadIdx.x == 0) s_live = 0;
     __syncthreads();  // sort outputs consumed / s_live cleared
     if (__ballot(thr < kThrDone) && lane == 0) atomicOr(&s_live, 1u << wv);
@@ -981,8 +988,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         uint64_t m = __ballot((s_u.st.q[lane] >> wv) & 1u);
         if (!((live >> wv) & 1u)) m = 0;
         // one entry's blend into this pixel's state (front to back)
-        auto take = [&](const Blend &e, float4 b, float4 c, int j) {
-            const bool ok = e.p2 <= 0.0f && e.alpha >= thr;  // blend_ok(e) for a live pixel
+        auto take = [&](const Blend &e, bool ok, float4 b, float4 c, int j) {
             const float test_T = fmaf(-e.alpha, Tt, Tt);  // T (1 - alpha), one rounding
             // keep == !(test_T < 1e-4) (test_T is never NaN: T in (0, 1], alpha in [0, 0.99]); the
             // pixel finishes when it takes the entry but may not keep it
@@ -1000,19 +1006,25 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const int j = __builtin_ctzll(m);
             m &= m - 1;
             const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
+            Blend e = blend_eval(a, b, pfx, pfy);
+            bool ok = e.p2 <= 0.0f && e.alpha >= thr;  // blend_ok(e) for a live pixel
             if constexpr (EXACT) {
-                Blend e = blend_eval(a, b, pfx, pfy);
-                const bool nr = thr < kThrDone && near_threshold(e.alpha);
-                if (__ballot(nr) && nr) {
+                // (one compare per evaluation; the re-evaluation is rare: ~6 % of the C3 tiles have one)
+                const bool nr = ok && e.alpha < kNearHi;
+                if (nr) {  // (an exec-masked region, skipped when no lane has one)
                     const int idx = base + j;
                     const uint32_t g = sorted_here ? (uint32_t)s_key[sort_slot(idx)] : point_list[rg.x + idx];
                     const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
                     e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
+                    ok = x.power <= 0.0f && x.alpha >= 1.0f / 255.0f;
+                    // the backward's walk of this tile looks the re-evaluated weight up (near_rec)
+                    const uint32_t slot = atomicAdd(&s_near, 1u);
+                    if (slot < kNearCap)
+                        near_rec[(size_t)kNearCap * tile + slot] =
+                            make_float4(__uint_as_float(((uint32_t)idx << 8) | pix_key), x.power, x.G, x.alpha);
                 }
-                take(e, b, c, j);
-            } else {
-                take(blend_eval(a, b, pfx, pfy), b, c, j);
             }
+            take(e, ok, b, c, j);
         }
         if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
@@ -1036,6 +1048,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     if ((lane & 31) == 0) atomicMax(&s_u.st.q[2 * (wv >> 1) + (lane >> 5)], mx);
     lds_barrier();  // the quarter maxima: no-return LDS atomics
     if (threadIdx.x < 4) tile_maxc[4 * tile + threadIdx.x] = s_u.st.q[threadIdx.x];
+    // near records of the tile (count; > kNearCap: the backward re-evaluates the tile itself)
+    if (threadIdx.x == 0) tile_flag[tile] = EXACT ? s_near : 0u;
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
 #endif
@@ -1159,7 +1173,7 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     k<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                         a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
                         a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
-                        a.gate_err, a.gate_timeout);
+                        a.gate_err, a.gate_timeout, a.tile_flag, a.near_rec);
     return hipGetLastError();
 }
 

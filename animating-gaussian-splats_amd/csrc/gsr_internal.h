@@ -19,6 +19,9 @@ struct FwdArgs {
     uint32_t *tile_order_f; uint32_t *seg_off; uint32_t *sort_lists; uint32_t *tile_count;
     uint32_t *tile_cursor; uint32_t *block_sums; uint32_t *block_off; uint32_t *meta; uint32_t *chunk_off;
     uint32_t *items_ws; uint32_t *scan_ws; uint32_t *tile_rank;
+    // exact-threshold mode: per tile, the count of near-threshold weights k_render_fwd re-evaluated, and
+    // their records (kNearCap per tile: key (list position << 8 | pixel), power, G, alpha)
+    uint32_t *tile_flag; float4 *near_rec;
     // binning
     uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
@@ -32,7 +35,8 @@ struct FwdArgs {
     // on when the speculation failed, the value that opens it, the forward's timeout error word (set to
     // gate_seq when the gate is abandoned) and the timeout (s_memrealtime ticks, 100 MHz)
     const uint32_t *gate; uint32_t gate_seq; uint32_t *gate_err; uint64_t gate_timeout;
-    // exact-threshold mode (gsr_set_exact_thresholds): near-threshold blend weights re-evaluated
+    // exact-threshold mode (gsr_set_exact_thresholds, on by default): near-threshold weights
+    // re-evaluated in the reference's expression order
     int exact;
 };
 // blocks of the speculative k_tile_sort launch (they loop over the device-side list count)
@@ -48,7 +52,7 @@ struct BwdArgs {
     // saved state
     const float4 *rec; const uint2 *rect; const uint8_t *clampm;
     const uint32_t *goff; const uint2 *ranges; const float4 *pix_end; const uint32_t *n_contrib;
-    const uint32_t *tile_maxc; const uint32_t *seg_off; const uint32_t *meta; uint32_t *items_ws;
+    const uint32_t *tile_maxc; const uint32_t *tile_flag; const float4 *near_rec; const uint32_t *seg_off; const uint32_t *meta; uint32_t *items_ws;
     const uint32_t *point_list; const uint32_t *slot_emit; const float4 *seg_state;
     uint2 *items; uint32_t max_items;
     // scratch
@@ -59,7 +63,6 @@ struct BwdArgs {
     float *dL_dmeans2D, *dL_dcolors, *dL_dopacity, *dL_dmeans3D, *dL_dcov3D, *dL_dsh, *dL_dscales,
         *dL_drot;
     int accm;  // gsr_grad_bits: outputs accumulated into instead of overwritten
-    int exact;  // exact-threshold mode (the forward's)
     const uint32_t *spec_ok;  // speculative render half (pair count unknown): kernels return when the forward's speculation failed
 };
 
@@ -75,8 +78,9 @@ hipError_t launch_mark_visible(int P, const float *means3D, const float *viewmat
                                hipStream_t s);
 
 hipError_t launch_bwd_items(const BwdArgs &a, hipStream_t s);
-hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc, uint2 *items,
-                                uint32_t *ws, hipStream_t s, const uint32_t *spec_ok = nullptr);
+hipError_t launch_bwd_items_raw(int K, int T, int P, const uint2 *ranges, const uint32_t *tile_maxc,
+                                const uint32_t *tile_flag, uint2 *items, uint32_t *ws, hipStream_t s,
+                                const uint32_t *spec_ok = nullptr);
 hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s);
 hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 // Each Gaussian's per-pair records of one view summed in emission order into kPartial x P SoA sums

@@ -188,15 +188,16 @@ def load_library():
     return L
 
 
-ABI_VERSION = 20  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
+ABI_VERSION = 21  # GSR_ABI_VERSION of include/gsr.h this binding's structs follow
 ACT_SIGMOID_OPACITY, ACT_EXP_SCALES, ACT_NORMALIZE_ROTATIONS = 1, 2, 4  # enum gsr_activation
 ACT_ALL = ACT_SIGMOID_OPACITY | ACT_EXP_SCALES | ACT_NORMALIZE_ROTATIONS
 
 
 def set_exact_thresholds(on: bool) -> bool:
-    """Exact-threshold mode (gsr_set_exact_thresholds, ABI 18): blend weights within 1e-5 of the 1/255
-    threshold re-evaluated in the reference's expression order, so the forward and backward take the
-    reference's decisions there.  Process-wide; returns the previous setting."""
+    """Exact-threshold mode (gsr_set_exact_thresholds; on by default since ABI 21): tiles where a blend
+    weight within 1e-5 of the 1/255 threshold was taken are redone with such weights re-evaluated in
+    the reference's expression order, so the forward and backward take the reference's decisions
+    there.  Process-wide; returns the previous setting."""
     return bool(load_library().gsr_set_exact_thresholds(int(bool(on))))
 
 
@@ -869,8 +870,8 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer, 
     """Typed views of the arrays inside the forward buffers (for parity tests / debugging);
     ``binning_layout``: the forward's info["binning_layout"] when it enqueued speculatively."""
     L = load_library()
-    offs = (ctypes.c_size_t * 14)()
-    L.gsr_buffer_offsets(int(P), int(W), int(H), int(binning_layout or num_rendered), offs, 14)
+    offs = (ctypes.c_size_t * 15)()
+    L.gsr_buffer_offsets(int(P), int(W), int(H), int(binning_layout or num_rendered), offs, 15)
     o = list(offs)
     T = ((W + 15) // 16) * ((H + 15) // 16)
     K = int(num_rendered)
@@ -897,6 +898,7 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer, 
         "seg_off": view(imgBuffer, o[12], T + 1, i32, (T + 1,)),
         "n_contrib": view(imgBuffer, o[7], W * H, i32, (H, W)),
         "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
+        "tile_flag": view(imgBuffer, o[14], T, i32, (T,)),  # 1: redone in the exact-threshold form
         # per-pair records (index, depth bits, emission, 0) in tile-bucket order; keys = .x | .y << 32
         "pairs": view(binningBuffer, o[9], 4 * K, i32, (K, 4)),
         "keys": view(binningBuffer, o[9], 2 * K, i64, (K, 2))[:, 0],

@@ -187,9 +187,10 @@ def set_speculative_forward(on: bool) -> bool:
 
 
 def set_exact_thresholds(on: bool) -> bool:
-    """Exact-threshold mode (include/gsr.h gsr_set_exact_thresholds): near-threshold blend weights
-    re-evaluated as the reference computes them (~15 % render-kernel time); returns the previous
-    setting.  Set it before a forward and keep it until that forward's backward has run."""
+    """Exact-threshold mode (include/gsr.h gsr_set_exact_thresholds, on by default): near-threshold
+    blend weights re-evaluated as the reference computes them, in the few tiles that have one;
+    returns the previous setting.  It applies to forwards queued after the call (a backward follows
+    the choice its forward made)."""
     return _C.set_exact_thresholds(on)
 
 

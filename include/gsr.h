@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define GSR_ABI_VERSION 20
+#define GSR_ABI_VERSION 21
 
 enum gsr_status {
     GSR_OK = 0,
@@ -322,22 +322,24 @@ size_t gsr_spec_binning_bytes(int P, int width, int height, int prepare_backward
  * pix_end (per pixel float4: accumulated colour without background, final transmittance),
  * n_contrib, tile_maxc}, binning {pairs (16-byte records: index, depth bits, emission, 0),
  * point_list, slot_emit}, image {seg_off}, binning {seg_state (the blend state at every interior
- * 128-entry boundary of every tile list: 256 float4 (C0, C1, C2, T) per boundary)}.  Returns the
- * count written (14). */
+ * 128-entry boundary of every tile list: 256 float4 (C0, C1, C2, T) per boundary)}, image
+ * {tile_flag (ABI 21: per tile, 1 when the forward redid it in the exact-threshold form)}.  Returns
+ * the count written (15, or max_out if smaller). */
 int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *out, int max_out);
 
 const char *gsr_last_error(void);
 int gsr_abi_version(void);
 
-/* Exact-threshold mode (ABI >= 18; process-wide, off by default, GSR_EXACT_THRESHOLDS=1 at load turns
- * it on).  The render kernels evaluate the blend weight as 2^(power log2 e) with FMAs and the hardware
- * exp, which differs from the reference's expf(power) (renderCUDA, forward.cu / backward.cu) by a few
- * ulp; a (pixel, Gaussian) weight that close to 1/255 can take the other side of the threshold.  With
- * the mode on, such weights (within 1e-5 relative of 1/255) are re-evaluated with the reference's
- * expression order and a double-precision exp, in the forward and the backward alike, so decisions
- * match the reference's (measured: blend-decision flips 1.5e-5 -> 0 of the pixels on the densest test
- * case) at ~15 % render-kernel time.  Set it before a forward and keep it until that
- * forward's backward has been queued.  Returns the previous setting. */
+/* Exact-threshold mode (ABI >= 18; process-wide; ON by default since ABI 21, GSR_EXACT_THRESHOLDS=0 at
+ * load turns it off).  The render kernels evaluate the blend weight as 2^(power log2 e) with FMAs and
+ * the hardware exp, which differs from the reference's expf(power) (renderCUDA, forward.cu /
+ * backward.cu) by a few ulp; a (pixel, Gaussian) weight that close to 1/255 can take the other side of
+ * the threshold.  With the mode on, k_render_fwd's fast pass notes whether any weight it took lies
+ * within 1e-5 (relative) of 1/255; such a tile (a few % of them) is redone at once with those weights
+ * re-evaluated in the reference's expression order and a double-precision exp, and its backward items
+ * run the same re-evaluation (IMAGE tile_flag), so decisions match the reference's.
+ * The backward follows the flags its forward wrote, so the setting may change at any time; it applies
+ * to forwards queued after the call.  Returns the previous setting. */
 int gsr_set_exact_thresholds(int on);
 
 /* ---- Fused L1 + SSIM image loss (ABI >= 3) ------------------------------

@@ -38,14 +38,14 @@ def test_library_exports_every_declared_symbol():
 
 def test_host_only_entry_points():
     L = _C.load_library()
-    assert L.gsr_abi_version() == _C.ABI_VERSION == 20
+    assert L.gsr_abi_version() == _C.ABI_VERSION == 21
     for P in (0, 1, 1000, 1_000_000):
         assert L.gsr_geom_bytes(P) % 256 == 0 and L.gsr_geom_bytes(P) >= 64 * P
     assert L.gsr_image_bytes(1920, 1080, 10) >= 1920 * 1080 * 8
     assert L.gsr_binning_bytes(100, 1000) >= 100 * 16 and L.gsr_scratch_bytes(100, 64, 48) >= 100 * 36
     assert L.gsr_sums_bytes(1000) >= 1000 * 36 and L.gsr_sums_bytes(1000) % 256 == 0  # ABI 15
-    offs = (ctypes.c_size_t * 14)()
-    assert L.gsr_buffer_offsets(100, 64, 48, 500, offs, 14) == 14
+    offs = (ctypes.c_size_t * 15)()
+    assert L.gsr_buffer_offsets(100, 64, 48, 500, offs, 15) == 15
     assert all(o % 256 == 0 for o in offs)
 
 

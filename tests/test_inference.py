@@ -5,7 +5,7 @@ create_extrinsic_matrices (train.py:459-503) at 1280 x 720, under ``torch.no_gra
 with ``Renderer(raster_settings=...)(**create_render_arguments(params))``: a forward-only call of the
 drop-in module on non-leaf activations.  Checked here on a 300k-Gaussian cloud:
 
-* radii bit-exact and colour / depth within 1e-4 (blend-threshold flips allowed at the headline's
+* radii bit-exact and colour / depth within 1e-4 (T-saturation flips allowed at 4x the measured
   rate) against the oracle, for every camera;
 * no per-call workspace outlives the call: with no autograd graph the GEOM / IMAGE / BINNING buffers
   (and any speculative BINNING) are released when the call returns, so the bytes requested from the
@@ -24,7 +24,7 @@ from test_gpu_parity import _close, _np
 pytestmark = pytest.mark.gpu
 
 P = 300_000
-PIX_FLIP = 4e-5  # blend decisions on a threshold (test_gpu_parity.py ALLOW, the C2-size cases)
+PIX_FLIP = 4.4e-6  # T >= 1e-4 saturation decisions: 4x the measured 1.09e-6 (profiles/r05_parity_flips.json)
 
 
 def _requested(dev):

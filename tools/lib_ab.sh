@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B library builds on the bench (headline + solo phases), alternated on one box.
 # usage: bash tools/lib_ab.sh OUTDIR REPS NAME...   (NAME = def -> the in-tree libgsr.so; NAMEtree -> the whole
-# exported tree tools/ab/NAMEtree (its own bench.py, package and libraries); else tools/ab/libgsr_NAME.so)
+# exported tree tools/ab/NAMEtree (its own bench.py, package and libraries); fast -> the in-tree library with
+# the exact-threshold mode off; else tools/ab/libgsr_NAME.so)
 set -u
 O=$1; N=$2; shift 2
 mkdir -p "$O"
@@ -10,6 +11,7 @@ for r in $(seq "$N"); do
   for v in "$@"; do
     case "$v" in
       def) GSR_LIB=animating-gaussian-splats_amd/diff_gaussian_rasterization/libgsr.so timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
+      fast) GSR_EXACT_THRESHOLDS=0 timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
       *tree) timeout -k 10 300 python -u tools/ab/$v/bench.py $LEGS > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
       *) GSR_LIB=tools/ab/libgsr_$v.so timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
     esac || { echo "bench $v failed"; tail -5 "$O/lab_$v$r.err"; exit 1; }
