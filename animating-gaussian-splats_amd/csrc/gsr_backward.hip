@@ -217,9 +217,9 @@ __device__ inline PairSums pair_sums(float S0, float S1, float S4, float cs0, fl
 }
 
 // Per-pixel walk state of one quarter slot k.
-struct PixState { float T, AR, d0, d1, d2, fy; int lrel; };
-// Running per-lane sums of one walked pair.
-struct LaneSums { float S0, S1, S4, c0, c1, c2; };
+struct PixState { float T, AR; f2v d01; float d2, fy; int lrel; };  // d01: dL/dpix channels 0, 1
+// Running per-lane sums of one walked pair (packed pairs: (S1, S4), (c0, c1)).
+struct LaneSums { float S0; f2v S14, c01; float c2; };
 
 // One (pair, quarter) evaluation.  CLAMP: the pair's opacity can exceed 0.99, so alpha may be clamped
 // (wave-uniform, flagged at staging); otherwise alpha = o G exactly and sG = o G T (C - AR) = w (C - AR)
@@ -266,7 +266,7 @@ __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &an
     any = any || ok;
     const float al = ok ? alpha : 0.f;
     ps.T = ps.T * __builtin_amdgcn_rcpf(1.f - al);  // T in front of the pair
-    const float cd = fmaf(c.z, ps.d2, fmaf(c.y, ps.d1, c.x * ps.d0));  // <colour, dL/dpix>
+    const float cd = fmaf(c.z, ps.d2, fmaf(c.y, ps.d01.y, c.x * ps.d01.x));  // <colour, dL/dpix>
     const float diff = cd - ps.AR;
     ps.AR = fmaf(al, diff, ps.AR);
     const float w = al * ps.T;
@@ -279,10 +279,8 @@ __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &an
     }
     const float u = gd * dy;
     s.S0 += gd;
-    s.S1 += u;
-    s.S4 = fmaf(u, dy, s.S4);
-    s.c0 = fmaf(w, ps.d0, s.c0);
-    s.c1 = fmaf(w, ps.d1, s.c1);
+    s.S14 = fma2(f2(gd, u), f2(dy, dy), s.S14);  // S1 += gd dy (fused), S4 += u dy
+    s.c01 = fma2(f2(w, w), ps.d01, s.c01);
     s.c2 = fmaf(w, ps.d2, s.c2);
 }
 
@@ -302,7 +300,7 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
         const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));
         const PairX x = pair_x(a, pfx);
         // -0 seeds: x + (-0) == x for every x, so the first contributor needs no add (the ISA folds it)
-        LaneSums s{-0.f, -0.f, -0.f, -0.f, -0.f, -0.f};
+        LaneSums s{-0.f, f2(-0.f, -0.f), f2(-0.f, -0.f), -0.f};
         bool any = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -312,7 +310,7 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
         // the skip pays although only ~3 % of the walked pairs have no taker (tools/contrib_stats.py):
         // always reducing measured 0.325 vs 0.316 ms alone (profiles/r05_bwd_micro_ab.txt)
         if (__builtin_amdgcn_ballot_w64(any)) {  // some pixel of the wave took the pair
-            const PairSums sm = pair_sums(s.S0, s.S1, s.S4, s.c0, s.c1, s.c2, x.dx, rw);
+            const PairSums sm = pair_sums(s.S0, s.S14.x, s.S14.y, s.c01.x, s.c01.y, s.c2, x.dx, rw);
             if ((threadIdx.x & 14) == 0) {  // lanes 0 and 1 of each row hold its two halves
                 float *o = o_row + j * kPartial;
                 lds_add(o, sm.X);
@@ -391,15 +389,14 @@ __device__ __forceinline__ void bwd_item(
         // entry p lies before the pixel's last contributor iff p < n_contrib: kept relative to the
         // batch start (lrel = n_contrib - start, advanced per batch)
         ps[k].lrel = (inside ? (int)n_contrib[pid] : 0) - s1;
-        ps[k].d0 = inside ? dL_dpixels[pid] : 0.f;
-        ps[k].d1 = inside ? dL_dpixels[H * W + pid] : 0.f;
+        ps[k].d01 = f2(inside ? dL_dpixels[pid] : 0.f, inside ? dL_dpixels[H * W + pid] : 0.f);
         ps[k].d2 = inside ? dL_dpixels[2 * H * W + pid] : 0.f;
         float bd = 0;
-        bd += bg0 * ps[k].d0; bd += bg1 * ps[k].d1; bd += bg2 * ps[k].d2;
+        bd += bg0 * ps[k].d01.x; bd += bg1 * ps[k].d01.y; bd += bg2 * ps[k].d2;
         if (has_bound && qmax[k] >= (uint32_t)s1f) {  // wave-uniform: this quarter resumes at the boundary
             const float4 st = seg_state[bidx + 64 * k + lane];
             ps[k].T = st.w;
-            const float behind = ps[k].d0 * (pe.x - st.x) + ps[k].d1 * (pe.y - st.y) + ps[k].d2 * (pe.z - st.z);
+            const float behind = ps[k].d01.x * (pe.x - st.x) + ps[k].d01.y * (pe.y - st.y) + ps[k].d2 * (pe.z - st.z);
             ps[k].AR = st.w > 0.f ? (behind + pe.w * bd) / st.w : bd;
         } else {
             ps[k].T = pe.w;

@@ -35,7 +35,7 @@ __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_
 // GEOM (per Gaussian, P): written by preprocess, read by binning/render/backward.
 //   rec: one 64-byte render record per Gaussian, so a (tile, Gaussian) gather touches one line:
 //        [0] = (x, y, A2, B2)        [1] = (C2, opacity, depth, tau2)
-//        [2] = (r, g, b, 0)          [3] = (conic_a, conic_b, conic_c, 0)
+//        [2] = (r, g, b, depth)      [3] = (conic_a, conic_b, conic_c, 0)
 //        power * log2(e) = A2 dx^2 + B2 dx dy + C2 dy^2, i.e. (A2, B2, C2) = -log2(e) (a/2, b, c/2),
 //        so the blend weight is one v_exp_f32; tau2 = 2 log2(255 opacity) bounds the alpha >= 1/255
 //        footprint (culling); [3] keeps the exact conic for gradients and introspection.
@@ -570,22 +570,31 @@ __device__ inline void trace_wave(uint64_t *buf, int slot, uint64_t t0, uint64_t
 // the backward (4 pixels of one column per lane) computes the dx-only part once per pair; forward
 // and backward use this exact operation sequence, hence bitwise-identical blend decisions.
 struct PairX { float dx, P0, P1; };
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ inline f2v f2(float x, float y) { return f2v{x, y}; }
 __device__ inline PairX pair_x(float4 r0, float pfx) {
     PairX x;
     x.dx = r0.x - pfx;
-    x.P0 = (r0.z * x.dx) * x.dx;
-    x.P1 = r0.w * x.dx;
+    const f2v t = f2(r0.z, r0.w) * f2(x.dx, x.dx);  // (A2 dx, B2 dx): one packed multiply
+    x.P0 = t.x * x.dx;
+    x.P1 = t.y;
     return x;
 }
 __device__ inline float pair_power(const PairX &x, float C2, float dy) { return fmaf(dy, fmaf(C2, dy, x.P1), x.P0); }
 
+// f2v (above): two-lane fp32 vectors -- the packed VALU forms (v_pk_add / v_pk_mul / v_pk_fma_f32) do
+// two of the same IEEE operations in one instruction, so the results are bitwise the scalar code's.
+__device__ inline f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
 struct Blend { float dx, dy, p2, G, alpha; };
 __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
     Blend e;
-    const PairX x = pair_x(r0, pfx);
-    e.dx = x.dx;
-    e.dy = r0.y - pfy;
-    e.p2 = pair_power(x, r1.x, e.dy);
+    // (dx, dy) and (A2 dx, B2 dx) as packed pairs: the same operations as pair_x / pair_power
+    const f2v d = f2(r0.x, r0.y) - f2(pfx, pfy);
+    const f2v t = f2(r0.z, r0.w) * f2(d.x, d.x);
+    e.dx = d.x;
+    e.dy = d.y;
+    e.p2 = fmaf(e.dy, fmaf(r1.x, e.dy, t.y), t.x * d.x);
     e.G = __builtin_amdgcn_exp2f(e.p2);
     e.alpha = fminf(0.99f, r1.y * e.G);
     return e;

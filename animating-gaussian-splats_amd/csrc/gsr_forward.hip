@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void k_preprocess(
     float4 *r = rec_out + (size_t)kRecF4 * i;
     r[0] = make_float4(pix_x, pix_y, -0.5f * GSR_LOG2E * ca, -GSR_LOG2E * cb);
     r[1] = make_float4(-0.5f * GSR_LOG2E * cc, o, pv.z, tau2);
-    r[2] = make_float4(rgb.x, rgb.y, rgb.z, 0.f);
+    r[2] = make_float4(rgb.x, rgb.y, rgb.z, pv.z);  // (.w: the depth again, beside the colour for the blend)
     r[3] = make_float4(ca, cb, cc, 0.f);
     rect_out[i] = pack_rect(x0, y0, x1, y1);
     tiles_out[i] = (uint32_t)((y1 - y0) * (x1 - x0));
@@ -861,8 +861,11 @@ __device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *e
     }
 }
 
+// 8 waves per SIMD (<= 64 VGPRs): the blend's latency is hidden by occupancy (6 waves: +17 %,
+// profiles/r05_fwd_ilp_ab.txt)
+#define GSR_FWD_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 template <bool EXACT>
-__global__ __launch_bounds__(256) void k_render_fwd(
+__global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     int W, int H, int gx, int T, const uint32_t *__restrict__ tile_order, const uint2 *__restrict__ ranges,
     const uint4 *__restrict__ pairs,
     uint32_t *__restrict__ point_list, uint32_t *__restrict__ slot_emit, const float4 *__restrict__ rec,
@@ -935,7 +938,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     if (threadIdx.x == 0) s_live = 0;
     __syncthreads();  // sort outputs consumed / s_live cleared
     if (__ballot(thr < kThrDone) && lane == 0) atomicOr(&s_live, 1u << wv);
-    float Tt = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, Dp = 0.f;
+    float Tt = 1.0f;
+    f2v C01 = f2(0.f, 0.f), C2D = f2(0.f, 0.f);  // (C0, C1), (C2, depth): packed accumulators
     uint32_t last = 0;
     // entry se of the NEXT batch: its render record halves (x, y, conic; colour) in registers, loaded
     // one batch ahead so the gathers' latency hides behind the current batch's blend
@@ -965,7 +969,7 @@ __global__ __launch_bounds__(256) void k_render_fwd(
         // which span two quarters; a finished pixel's state is its final one)
         if (base > 0 && (base & ((1 << ks) - 1)) == 0) {
             const size_t b = (size_t)seg_off[tile] + ((uint32_t)base >> ks) - 1u;
-            seg_state[b * kTilePix + bslot] = make_float4(C0, C1, C2, Tt);
+            seg_state[b * kTilePix + bslot] = make_float4(C01.x, C01.y, C2D.x, Tt);
         }
         // ---- stage the batch (block-wide) ----
         bool hit = false;
@@ -995,10 +999,8 @@ __global__ __launch_bounds__(256) void k_render_fwd(
             const bool use = ok && test_T >= 0.0001f;
             thr = (ok && !use) ? kThrDone : thr;
             const float w = use ? e.alpha * Tt : 0.f;
-            C0 = fmaf(c.x, w, C0);
-            C1 = fmaf(c.y, w, C1);
-            C2 = fmaf(c.z, w, C2);
-            Dp = fmaf(b.z, w, Dp);
+            C01 = fma2(f2(c.x, c.y), f2(w, w), C01);  // C0, C1 += (c.x, c.y) w
+            C2D = fma2(f2(c.z, c.w), f2(w, w), C2D);  // C2, depth += (c.z, depth) w
             Tt = use ? test_T : Tt;
             last = use ? (uint32_t)(base + j + 1) : last;
         };
@@ -1030,12 +1032,12 @@ __global__ __launch_bounds__(256) void k_render_fwd(
     }
     if (inside) {
         const int pid = py * W + px;
-        pix_end[pid] = make_float4(C0, C1, C2, Tt);
+        pix_end[pid] = make_float4(C01.x, C01.y, C2D.x, Tt);
         n_contrib[pid] = last;
-        out_color[pid] = C0 + Tt * bg[0];
-        out_color[H * W + pid] = C1 + Tt * bg[1];
-        out_color[2 * H * W + pid] = C2 + Tt * bg[2];
-        out_depth[pid] = Dp;
+        out_color[pid] = C01.x + Tt * bg[0];
+        out_color[H * W + pid] = C01.y + Tt * bg[1];
+        out_color[2 * H * W + pid] = C2D.x + Tt * bg[2];
+        out_depth[pid] = C2D.y;
     }
     // per 16x4 strip maximum of n_contrib (the backward's quarters): rows 4k..4k+3 = half of the lanes of
     // two waves; lanes (lane >> 3) < 4 hold strip 2 (wv >> 1), the others strip 2 (wv >> 1) + 1

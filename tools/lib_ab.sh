@@ -11,6 +11,7 @@ for r in $(seq "$N"); do
   for v in "$@"; do
     case "$v" in
       def) GSR_LIB=animating-gaussian-splats_amd/diff_gaussian_rasterization/libgsr.so timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
+      *_fast) GSR_EXACT_THRESHOLDS=0 GSR_LIB=tools/ab/libgsr_${v%_fast}.so timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
       fast) GSR_EXACT_THRESHOLDS=0 timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
       *tree) timeout -k 10 300 python -u tools/ab/$v/bench.py $LEGS > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
       *) GSR_LIB=tools/ab/libgsr_$v.so timeout -k 10 300 python -u bench.py $LEGS --inference-steps 0 > "$O/lab_$v$r.json" 2> "$O/lab_$v$r.err" ;;
@@ -18,6 +19,6 @@ for r in $(seq "$N"); do
     python3 -c "
 import json; d=json.loads(open('$O/lab_$v$r.json').read().strip().splitlines()[-1])
 s=d['phase_ms_per_launch_solo']
-print('$v', d['value'], d['median_ms_per_step'], 'solo fwd/bwd', s['render_fwd'], s['render_bwd'], 'step bwd', d['phase_ms_per_launch']['render_bwd'])"
+print('$v', d['value'], d['median_ms_per_step'], 'solo pre/fwd/bwd/gbwd', s['preprocess'], s['render_fwd'], s['render_bwd'], s['gauss_bwd'], 'step bwd', d['phase_ms_per_launch']['render_bwd'])"
   done
 done
