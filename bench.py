@@ -38,9 +38,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh): HBM bytes per
 # launch of each kernel, converted per access shape (calibrated_traffic; MI355X_MICROARCH.md's 2 x
 # FETCH_SIZE + WRITE_SIZE is the streaming case and is reported beside it)
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r04_hbm_pmc.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r05_hbm_pmc.json")
 # SQ counters of the same command (tools/profile_round.sh sq passes): VALU activity per launch
-SQ_SUMMARY = os.path.join(REPO, "profiles", "r04_sq_pmc.json")
+SQ_SUMMARY = os.path.join(REPO, "profiles", "r05_sq_pmc.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
 PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "bwd_items",
           "render_bwd", "sum_records", "gauss_bwd"]
