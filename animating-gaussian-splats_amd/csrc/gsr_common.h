@@ -587,6 +587,8 @@ __device__ inline float pair_power(const PairX &x, float C2, float dy) { return 
 __device__ inline f2v fma2(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
 
 struct Blend { float dx, dy, p2, G, alpha; };
+// CLAMP = false: no staged opacity exceeds 0.99, so min(0.99, o G) == o G wherever p2 <= 0 (G <= 1)
+template <bool CLAMP = true>
 __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
     Blend e;
     // (dx, dy) and (A2 dx, B2 dx) as packed pairs: the same operations as pair_x / pair_power
@@ -596,7 +598,7 @@ __device__ inline Blend blend_eval(float4 r0, float4 r1, float pfx, float pfy) {
     e.dy = d.y;
     e.p2 = fmaf(e.dy, fmaf(r1.x, e.dy, t.y), t.x * d.x);
     e.G = __builtin_amdgcn_exp2f(e.p2);
-    e.alpha = fminf(0.99f, r1.y * e.G);
+    e.alpha = CLAMP ? fminf(0.99f, r1.y * e.G) : r1.y * e.G;
     return e;
 }
 __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha >= 1.0f / 255.0f; }

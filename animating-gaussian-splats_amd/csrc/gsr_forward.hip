@@ -22,6 +22,7 @@
 #include "gsr_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace gsr {
 
@@ -972,9 +973,10 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
             seg_state[b * kTilePix + bslot] = make_float4(C01.x, C01.y, C2D.x, Tt);
         }
         // ---- stage the batch (block-wide) ----
-        bool hit = false;
+        bool hit = false, opaque = false;
         {   // this batch's records were loaded during the previous batch's blend
             const float4 a = pa, b = pb;
+            opaque = pv && b.y > 0.99f;  // alpha = min(0.99, o G) can clamp
             if (pv) {
                 if (sq < 3) s_u.st.rec[sq][se] = pr;
                 hit = ((live >> sq) & 1u) &&
@@ -986,11 +988,14 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
         uint32_t bits = hit ? (1u << sq) : 0u;
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xF, 0xF, false);  // xor 1
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xF, 0xF, false);  // xor 2
-        if (sq == 0) s_u.st.q[se] = bits;
+        if (sq == 0) s_u.st.q[se] = bits | ((bits && opaque) ? 16u : 0u);  // bit 4: a clamping entry
         __syncthreads();
         // ---- blend this wave's quarter ----
-        uint64_t m = __ballot((s_u.st.q[lane] >> wv) & 1u);
+        const uint32_t qw = s_u.st.q[lane];
+        uint64_t m = __ballot((qw >> wv) & 1u);
         if (!((live >> wv) & 1u)) m = 0;
+        // batch-uniform: some staged entry's opacity exceeds 0.99 (the backward takes the same variant)
+        const bool clamp = __builtin_amdgcn_ballot_w64((qw & 16u) != 0u) != 0;
         // one entry's blend into this pixel's state (front to back)
         auto take = [&](const Blend &e, bool ok, float4 b, float4 c, int j) {
             const float test_T = fmaf(-e.alpha, Tt, Tt);  // T (1 - alpha), one rounding
@@ -1004,30 +1009,35 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
             Tt = use ? test_T : Tt;
             last = use ? (uint32_t)(base + j + 1) : last;
         };
-        while (m) {
-            const int j = __builtin_ctzll(m);
-            m &= m - 1;
-            const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
-            Blend e = blend_eval(a, b, pfx, pfy);
-            bool ok = e.p2 <= 0.0f && e.alpha >= thr;  // blend_ok(e) for a live pixel
-            if constexpr (EXACT) {
-                // (one compare per evaluation; the re-evaluation is rare: ~6 % of the C3 tiles have one)
-                const bool nr = ok && e.alpha < kNearHi;
-                if (nr) {  // (an exec-masked region, skipped when no lane has one)
-                    const int idx = base + j;
-                    const uint32_t g = sorted_here ? (uint32_t)s_key[sort_slot(idx)] : point_list[rg.x + idx];
-                    const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
-                    e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
-                    ok = x.power <= 0.0f && x.alpha >= 1.0f / 255.0f;
-                    // the backward's walk of this tile looks the re-evaluated weight up (near_rec)
-                    const uint32_t slot = atomicAdd(&s_near, 1u);
-                    if (slot < kNearCap)
-                        near_rec[(size_t)kNearCap * tile + slot] =
-                            make_float4(__uint_as_float(((uint32_t)idx << 8) | pix_key), x.power, x.G, x.alpha);
+        auto walk = [&](auto clamp_c) {
+            constexpr bool CL = decltype(clamp_c)::value;
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
+                Blend e = blend_eval<CL>(a, b, pfx, pfy);
+                bool ok = e.p2 <= 0.0f && e.alpha >= thr;  // blend_ok(e) for a live pixel
+                if constexpr (EXACT) {
+                    // (one compare per evaluation; the re-evaluation is rare: ~6 % of the C3 tiles have one)
+                    const bool nr = ok && e.alpha < kNearHi;
+                    if (nr) {  // (an exec-masked region, skipped when no lane has one)
+                        const int idx = base + j;
+                        const uint32_t g = sorted_here ? (uint32_t)s_key[sort_slot(idx)] : point_list[rg.x + idx];
+                        const ExactBlend x = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * g + 3], b.y, pfx, pfy);
+                        e.p2 = x.power; e.G = x.G; e.alpha = x.alpha;
+                        ok = x.power <= 0.0f && x.alpha >= 1.0f / 255.0f;
+                        // the backward's walk of this tile looks the re-evaluated weight up (near_rec)
+                        const uint32_t slot = atomicAdd(&s_near, 1u);
+                        if (slot < kNearCap)
+                            near_rec[(size_t)kNearCap * tile + slot] =
+                                make_float4(__uint_as_float(((uint32_t)idx << 8) | pix_key), x.power, x.G, x.alpha);
+                    }
                 }
+                take(e, ok, b, c, j);
             }
-            take(e, ok, b, c, j);
-        }
+        };
+        if (clamp) walk(std::true_type{});
+        else walk(std::false_type{});
         if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
     if (inside) {
