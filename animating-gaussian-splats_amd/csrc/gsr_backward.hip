@@ -165,10 +165,11 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
     d[2] = F3{r6, r7, r8};
 }
 
-// the register budget: 6 waves per SIMD (80 VGPRs, no spills since the record inputs wait in LDS;
-// 3 % faster alone than 5 waves, profiles/r05_bwd_waves_ab.txt); the exact-threshold variant keeps 5
-// (96 VGPRs: its near-threshold call site needs the registers)
-#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 4 : 6, 8)))
+// the register budget: 7 waves per SIMD (72 VGPRs, LDS 21.5 KB per 4-wave workgroup; the record's two
+// tail inputs live in a register pair that the compiler parks in scratch during the walk: one store and
+// one load per batch).  1 % faster alone than 6 waves (profiles/r05_bwd_waves_ab.txt; 5 -> 6 was 3 %).
+// The near-overflow variant keeps 4 (its re-evaluation call site needs the registers).
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 4 : 7, 8)))
 constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
 constexpr int kExactBwdBlocks = 256;  // grid of the exact-threshold tiles' k_render_bwd
 
@@ -322,9 +323,9 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
 }
 
 // One (tile, segment) item of k_render_bwd on one wave, with the wave's LDS slices: per staged entry
-// (x, y, A2, B2); + kStage: (C2, opacity, exact conic a, b); + 2 kStage: colour + quarter mask; s_tail:
-// (exact conic c, emission index) -- the record's inputs wait in LDS, not in registers, while the
-// batch is walked.
+// (x, y, A2, B2); + kStage: (C2, opacity, exact conic a, b); + 2 kStage: colour + quarter mask -- the
+// record's inputs wait in LDS, not in registers, while the batch is walked (but for the exact conic's
+// c and the emission index, which the staging lane keeps).
 template <bool EXACT>
 __device__ __forceinline__ void bwd_item(
     uint2 it, uint32_t item, int W, int H, int gx, const uint2 *__restrict__ ranges,
@@ -334,7 +335,7 @@ __device__ __forceinline__ void bwd_item(
     const uint32_t *__restrict__ seg_off, const float4 *__restrict__ seg_state,
     const uint32_t *__restrict__ slot_emit, const float *__restrict__ dL_dpixels,
     float4 *__restrict__ part, int ks, const uint32_t *__restrict__ tile_flag,
-    const float4 *__restrict__ near_rec, float4 *s_a, float2 *s_tail, float *s_out) {
+    const float4 *__restrict__ near_rec, float4 *s_a, float *s_out) {
     constexpr int kStage = 64 * kBwdWaves;
 #ifdef GSR_TRACE
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
@@ -422,10 +423,11 @@ __device__ __forceinline__ void bwd_item(
         const int start = end - 64 > s0 ? end - 64 : s0;
         const int cnt = end - start;
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, cj = a;
+        float2 tl = make_float2(0.f, 0.f);
         if (lane < cnt) {
             const float4 *r = rec + (size_t)kRecF4 * g_n;
             a = r[0]; b = r[1]; c = r[2]; cj = r[3];  // cj: exact conic (a, b, c) of the staged Gaussian
-            s_tail[lane] = make_float2(cj.z, __uint_as_float(em_n));
+            tl = make_float2(cj.z, __uint_as_float(em_n));
         }
         if (end - 64 > s0) fetch(end - 64);
 #pragma unroll
@@ -472,7 +474,7 @@ __device__ __forceinline__ void bwd_item(
 #pragma unroll
             for (int q = 0; q < kPartial; ++q) sm[q] = s2[q];
             const float4 bj = s_a[kStage + lane];  // (C2, opacity, exact conic a, b)
-            const float2 tl = s_tail[lane];         // (exact conic c, emission index)
+            // tl: (exact conic c, emission index) of the entry this lane staged
             const float o = bj.y;
             const uint32_t em = __float_as_uint(tl.y);
             // sums of sG = o G dL/dalpha: the opacity is already in; dL/dopacity = sum G dL/dalpha
@@ -512,23 +514,21 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     // (one address VGPR per pair, the rest immediate offsets).
     constexpr int kStage = 64 * kBwdWaves;
     __shared__ float4 s_stage[3 * kStage];
-    __shared__ float2 s_tail_all[kStage];  // per staged entry: (exact conic c, emission index) for the record
     __shared__ float s_out_all[64 * kPartial * kBwdWaves];  // per staged pair: its kPartial wave sums
     if (spec_ok && *spec_ok == 0u) return;  // speculative render half whose forward was redone: redone too
     // (the wave index as a scalar: the item, its tile and everything derived from them live in SGPRs)
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4 *s_a = s_stage + 64 * wv;
-    float2 *s_tail = s_tail_all + 64 * wv;
     float *s_out = s_out_all + 64 * kPartial * wv;
     const uint2 hd = items[0];  // (items, items of the tiles with more than kNearCap near records after them)
     if constexpr (EXACT) {
         // the tiles with more near-threshold weights than kNearCap (rare): every wave loops over them
         for (uint32_t i = blockIdx.x * kBwdWaves + wv; i < hd.y; i += gridDim.x * kBwdWaves)
-            bwd_item<true>(items[1 + hd.x + i], hd.x + i, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_tail, s_out);
+            bwd_item<true>(items[1 + hd.x + i], hd.x + i, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_out);
     } else {
         const uint32_t item = blockIdx.x * kBwdWaves + wv;
         if (item >= hd.x) return;  // the launch covers the item bound
-        bwd_item<false>(items[1 + item], item, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_tail, s_out);
+        bwd_item<false>(items[1 + item], item, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_out);
     }
 }
 
