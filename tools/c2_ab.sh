@@ -7,9 +7,11 @@ for r in $(seq "$N"); do
   for v in "$@"; do
     case "$v" in
       def|fast) B="bench.py $EXTRA_DEF" ;;
+      lib_*) B="bench.py $EXTRA_DEF" ;;
       *) B=tools/ab/$v/bench.py ;;
     esac
     if [ "$v" = fast ]; then B="bench.py $EXTRA_DEF"; export GSR_EXACT_THRESHOLDS=0; else unset GSR_EXACT_THRESHOLDS; fi
+    case "$v" in lib_*) export GSR_LIB=tools/ab/libgsr_${v#lib_}.so ;; *) unset GSR_LIB ;; esac
     timeout -k 10 300 python -u $B $LEGS > "$O/c2_$v$r.json" 2> "$O/c2_$v$r.err" || { echo "bench $v failed"; tail -3 "$O/c2_$v$r.err"; exit 1; }
     python3 -c "
 import json; d=json.loads(open('$O/c2_$v$r.json').read().strip().splitlines()[-1]); c=d['c2']
