@@ -834,6 +834,9 @@ __device__ inline void view_chain(float3 mean, const float (&c3)[6], const float
     dm2 += (pj[8] * m_w - pj[11] * mul1) * g2x + (pj[9] * m_w - pj[11] * mul2) * g2y;
 }
 
+// A Gaussian's inputs that k_gauss_bwd loads before its record walk (their latency overlaps it).
+struct GaussIn { int radius; float3 mean, s3; float4 q; float o; };
+
 template <int MC>
 __device__ inline void gauss_bwd_one(
     int i, int D, int M, int W, int H, float scale_modifier, float tan_fovx, float tan_fovy,
@@ -845,13 +848,13 @@ __device__ inline void gauss_bwd_one(
     float *__restrict__ dL_dcolors, float *__restrict__ dL_dopacity, float *__restrict__ dL_dmeans3D,
     float *__restrict__ dL_dcov3D, float *__restrict__ dL_dsh, float *__restrict__ dL_dscales,
     float *__restrict__ dL_drot, float *s_row, int act, const float4 *__restrict__ rec, int accm,
-    const uint8_t *__restrict__ clampm) {
+    const uint8_t *__restrict__ clampm, const GaussIn &gi) {
     // every output may be NULL (gradient not requested: the input does not require grad); accm:
     // gsr_grad_bits of the outputs to add into instead of overwrite
     const bool a2 = accm & GSR_GRAD_MEANS2D, ac = accm & GSR_GRAD_COLORS, ao = accm & GSR_GRAD_OPACITY,
                a3 = accm & GSR_GRAD_MEANS3D, acv = accm & GSR_GRAD_COV3D, ash = accm & GSR_GRAD_SH,
                asc = accm & GSR_GRAD_SCALES, ar = accm & GSR_GRAD_ROTATIONS;
-    if (!(radii[i] > 0)) {  // zero gradient: accumulated outputs keep their content
+    if (!(gi.radius > 0)) {  // zero gradient: accumulated outputs keep their content
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             if (dL_dmeans2D && !a2) dL_dmeans2D[3 * i + k] = 0.f;
@@ -888,7 +891,7 @@ __device__ inline void gauss_bwd_one(
         // opacity = sigmoid(logit) when fused: d/dlogit = o (1 - o), o from the forward's record
         if (!dL_dopacity) {
         } else if (act & GSR_ACT_SIGMOID_OPACITY) {
-            const float o = rec[(size_t)kRecF4 * i + 1].y;
+            const float o = gi.o;
             gput_old(dL_dopacity, i, acc[5] * ((1.f - o) * o), ao, oo[0]);
         } else {
             gput_old(dL_dopacity, i, acc[5], ao, oo[0]);
@@ -901,7 +904,7 @@ __device__ inline void gauss_bwd_one(
     float vm[16], pj[16];
     load_mat16(viewmatrix, cs.v0, cs.v1, vm);
     load_mat16(projmatrix, cs.p0, cs.p1, pj);
-    const float3 mean = make_float3(means3D[3 * i], means3D[3 * i + 1], means3D[3 * i + 2]);
+    const float3 mean = gi.mean;
     float c3[6];
     float3 s3 = make_float3(0, 0, 0);
     float4 q = make_float4(0, 0, 0, 0);
@@ -910,8 +913,8 @@ __device__ inline void gauss_bwd_one(
 #pragma unroll
         for (int k = 0; k < 6; ++k) c3[k] = cov3D_precomp[6 * i + k];
     } else {
-        s3 = make_float3(scales[3 * i], scales[3 * i + 1], scales[3 * i + 2]);
-        q = make_float4(rotations[4 * i], rotations[4 * i + 1], rotations[4 * i + 2], rotations[4 * i + 3]);
+        s3 = gi.s3;
+        q = gi.q;
         if (act & GSR_ACT_EXP_SCALES) s3 = act_exp3(s3);
         if (act & GSR_ACT_NORMALIZE_ROTATIONS) { qn = quat_norm(q); q = act_normalize(q, qn); }
         cov3d_from_scale_rot(s3, scale_modifier, q, c3);
@@ -985,7 +988,20 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
     const int i0 = blockIdx.x * kShBlock;
     const int nrow = min(kShBlock, P - i0);
     const int i = i0 + threadIdx.x;
-    // the record sums first, each wave in its own slice of the block's LDS (which the SH rows reuse)
+    // the Gaussian's radius, parameters and activated opacity are loaded first (clamped index for the
+    // tail lanes), so their latency overlaps the record walk instead of following it
+    const int ic = min(i, P - 1);
+    GaussIn gi;
+    gi.radius = radii[ic];
+    gi.mean = make_float3(means3D[3 * ic], means3D[3 * ic + 1], means3D[3 * ic + 2]);
+    gi.s3 = make_float3(0.f, 0.f, 0.f);
+    gi.q = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!cov3D_precomp) {
+        gi.s3 = make_float3(scales[3 * ic], scales[3 * ic + 1], scales[3 * ic + 2]);
+        gi.q = make_float4(rotations[4 * ic], rotations[4 * ic + 1], rotations[4 * ic + 2], rotations[4 * ic + 3]);
+    }
+    gi.o = (act & GSR_ACT_SIGMOID_OPACITY) && dL_dopacity ? rec[(size_t)kRecF4 * ic + 1].y : 0.f;
+    // the record sums, each wave in its own slice of the block's LDS (which the SH rows reuse)
     float acc[kPartial];
     sum_records_wave<MC>(i, P, goff, part, reinterpret_cast<float4 *>(s_sh) + (threadIdx.x >> 6) * kRecStageF4<MC>, acc);
     if constexpr (MC > 0) {  // coalesced copy of this block's SH rows into LDS (reused for dL/dSH)
@@ -997,7 +1013,7 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
                                  scales, rotations, shs, cov3D_precomp, viewmatrix, projmatrix, campos, cs,
                                  radii, acc, dL_dmeans2D, dL_dcolors, dL_dopacity,
                                  dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drot, s_sh + threadIdx.x * RS,
-                                 act, rec, accm, clampm);
+                                 act, rec, accm, clampm, gi);
     if constexpr (MC > 0) {  // coalesced store of the dL/dSH rows
         if (!dL_dsh) return;
         __syncthreads();
@@ -1055,10 +1071,8 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     const bool live = i < P;
     const int ii = live ? i : i0;  // lanes past P load (and never store) row i0's parameters
     float *s_row = s_sh + threadIdx.x * RS;
-    if constexpr (MC > 0) {  // coefficient rows, read by every view's SH chain
-        sh_rows_to_lds<MC>(a.shs + (size_t)i0 * RL, nrow, s_sh);
-        __syncthreads();
-    }
+    // the Gaussian's own parameters and the first view's record sums and radius are loaded before the
+    // SH row copy, so that their latency overlaps it instead of following its barrier
     const float3 mean = make_float3(a.means3D[3 * ii], a.means3D[3 * ii + 1], a.means3D[3 * ii + 2]);
     float c3[6];
     float3 s3 = make_float3(0, 0, 0);
@@ -1070,6 +1084,18 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     } else {
         s3 = make_float3(a.scales[3 * ii], a.scales[3 * ii + 1], a.scales[3 * ii + 2]);
         q = make_float4(a.rotations[4 * ii], a.rotations[4 * ii + 1], a.rotations[4 * ii + 2], a.rotations[4 * ii + 3]);
+    }
+    // each view's record sums (gsr_backward_render's k_sum_records, kPartial x P SoA: coalesced) and
+    // radius are loaded one view ahead, so their latency hides behind the previous view's chains
+    float nx[kPartial];
+#pragma unroll
+    for (int k = 0; k < kPartial; ++k) nx[k] = a.v[0].sums[(size_t)k * P + ii];
+    int rn = a.v[0].radii[ii];
+    if constexpr (MC > 0) {  // coefficient rows, read by every view's SH chain
+        sh_rows_to_lds<MC>(a.shs + (size_t)i0 * RL, nrow, s_sh);
+        __syncthreads();
+    }
+    if (!a.cov3D_precomp) {
         if (a.act & GSR_ACT_EXP_SCALES) s3 = act_exp3(s3);
         if (a.act & GSR_ACT_NORMALIZE_ROTATIONS) { qn = quat_norm(q); q = act_normalize(q, qn); }
         cov3d_from_scale_rot(s3, a.scale_modifier, q, c3);
@@ -1080,12 +1106,6 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     float o_act = 0.f;  // the activated opacity, from the record of a view that sees the Gaussian
     float m2[3] = {0.f, 0.f, 0.f};  // the screen-space gradient carried across views of one array
     const int active = (a.D + 1) * (a.D + 1);
-    // each view's record sums (gsr_backward_render's k_sum_records, kPartial x P SoA: coalesced) and
-    // radius are loaded one view ahead, so their latency hides behind the previous view's chains
-    float nx[kPartial];
-#pragma unroll
-    for (int k = 0; k < kPartial; ++k) nx[k] = a.v[0].sums[(size_t)k * P + ii];
-    int rn = a.v[0].radii[ii];
     for (int v = 0; v < a.nv; ++v) {
         const MultiView &V = a.v[v];
         const int rv = rn;
@@ -1217,18 +1237,31 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if (live) {
 #pragma unroll
             for (int k = 0; k < RL; ++k) s_row[k] = 0.f;
+            // a view's radius, clamp mask and colour sums are loaded together (none waits for the
+            // radius) and one view ahead, so the loop pays one load latency instead of two per view
+            int rv_n = a.v[0].radii[i];
+            uint8_t cm_n = a.v[0].clampm[i];
+            float g_n[3] = {a.v[0].sums[(size_t)6 * P + i], a.v[0].sums[(size_t)7 * P + i], a.v[0].sums[(size_t)8 * P + i]};
             for (int v = 0; v < a.nv; ++v) {
                 const MultiView &V = a.v[v];
-                if (!(V.radii[i] > 0)) continue;
+                const int rv = rv_n;
+                const uint8_t cm = cm_n;
+                const float g[3] = {g_n[0], g_n[1], g_n[2]};
+                if (v + 1 < a.nv) {
+                    const MultiView &Vn = a.v[v + 1];
+                    rv_n = Vn.radii[i];
+                    cm_n = Vn.clampm[i];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) g_n[c] = Vn.sums[(size_t)(6 + c) * P + i];
+                }
+                if (!(rv > 0)) continue;
                 const float3 cp = load_campos(V.campos, V.cs.c0);
                 bool cl[3];
-                clamp_from_mask(V.clampm[i], cl);
+                clamp_from_mask(cm, cl);
                 const float3 d0 = make_float3(mean.x - cp.x, mean.y - cp.y, mean.z - cp.z);
                 const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
                 const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
-                const float dRGB[3] = {V.sums[(size_t)6 * P + i] * (cl[0] ? 0.f : 1.f),
-                                       V.sums[(size_t)7 * P + i] * (cl[1] ? 0.f : 1.f),
-                                       V.sums[(size_t)8 * P + i] * (cl[2] ? 0.f : 1.f)};
+                const float dRGB[3] = {g[0] * (cl[0] ? 0.f : 1.f), g[1] * (cl[1] ? 0.f : 1.f), g[2] * (cl[2] ? 0.f : 1.f)};
                 float basis[16];
                 sh_basis16(x, y, z, basis);
 #pragma unroll
