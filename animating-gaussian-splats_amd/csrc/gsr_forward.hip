@@ -1003,11 +1003,13 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
             // pixel finishes when it takes the entry but may not keep it
             const bool use = ok && test_T >= 0.0001f;
             thr = (ok && !use) ? kThrDone : thr;
-            const float w = use ? e.alpha * Tt : 0.f;
-            C01 = fma2(f2(c.x, c.y), f2(w, w), C01);  // C0, C1 += (c.x, c.y) w
-            C2D = fma2(f2(c.z, c.w), f2(w, w), C2D);  // C2, depth += (c.z, depth) w
-            Tt = use ? test_T : Tt;
-            last = use ? (uint32_t)(base + j + 1) : last;
+            if (use) {  // an exec-masked update: no selects for w, T and the last contributor (-1 %)
+                const float w = e.alpha * Tt;
+                C01 = fma2(f2(c.x, c.y), f2(w, w), C01);  // C0, C1 += (c.x, c.y) w
+                C2D = fma2(f2(c.z, c.w), f2(w, w), C2D);  // C2, depth += (c.z, depth) w
+                Tt = test_T;
+                last = (uint32_t)(base + j + 1);
+            }
         };
         auto walk = [&](auto clamp_c) {
             constexpr bool CL = decltype(clamp_c)::value;
