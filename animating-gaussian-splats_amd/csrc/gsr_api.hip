@@ -269,7 +269,8 @@ size_t gsr_binning_bytes(int K, int P) { return BinningLayout(K, P).total; }
 size_t gsr_backward_items_bytes(int K, int W, int H) {
     return bwd_items_bytes(K < 0 ? 0 : K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH));
 }
-size_t gsr_sums_bytes(int P) { return align256(sizeof(float) * kPartial * (size_t)(P < 0 ? 0 : P)); }
+// kPartial x P sums, then the view's camera key (k_sum_records; the multi-view pass orders views by it)
+size_t gsr_sums_bytes(int P) { return align256(sizeof(float) * (kPartial * (size_t)(P < 0 ? 0 : P) + 1)); }
 size_t gsr_scratch_bytes(int K, int W, int H) {
     return ScratchLayout(K, div_up(W < 0 ? 0 : W, kTileW) * div_up(H < 0 ? 0 : H, kTileH)).total;
 }
@@ -1015,7 +1016,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
         float *out = (float *)alloc(alloc_ctx, GSR_BUF_SUMS, gsr_sums_bytes(a.P));
         if (!out) return fail(GSR_ERR_ALLOC, "allocation callback failed (sums)");
         Phase ph(s, "sum_records");
-        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s, a.spec_ok));
+        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s, a.spec_ok, a.viewmatrix, a.campos, a.cs));
     }
     return GSR_OK;
 }

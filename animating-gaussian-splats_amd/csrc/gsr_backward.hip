@@ -1030,11 +1030,27 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // of LDS per wave, so the walk's LDS round trips hide behind other waves; it runs on the view's
 // stream right after k_render_bwd, beside the other views' render kernels.
 constexpr int kSumChunk = 128;
+// The view's camera key (FNV-1a over the bits of its view matrix and camera position), stored after the
+// sums: k_gauss_bwd_multi orders a launch's views by it (view_order).
+__device__ inline uint32_t camera_key(const float *viewmatrix, const float *campos, CamStrides cs) {
+    float vm[16];
+    load_mat16(viewmatrix, cs.v0, cs.v1, vm);
+    const float3 cp = load_campos(campos, cs.c0);
+    const float w[19] = {vm[0], vm[1], vm[2], vm[3], vm[4], vm[5], vm[6], vm[7], vm[8], vm[9], vm[10], vm[11],
+                         vm[12], vm[13], vm[14], vm[15], cp.x, cp.y, cp.z};
+    uint32_t x = 2166136261u;
+#pragma unroll
+    for (int k = 0; k < 19; ++k) x = (x ^ __float_as_uint(w[k])) * 16777619u;
+    return x;
+}
 __global__ __launch_bounds__(256) void k_sum_records(int P, const uint32_t *__restrict__ goff,
                                                      const float4 *__restrict__ part, float *__restrict__ sums,
-                                                     const uint32_t *__restrict__ spec_ok) {
+                                                     const uint32_t *__restrict__ spec_ok, const float *viewmatrix,
+                                                     const float *campos, CamStrides cs) {
     __shared__ float4 s_stage[3 * kSumChunk * 4];
     if (spec_ok && *spec_ok == 0u) return;  // (as k_render_bwd)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        reinterpret_cast<uint32_t *>(sums)[(size_t)kPartial * P] = camera_key(viewmatrix, campos, cs);
     const int i = blockIdx.x * 256 + threadIdx.x;
     float acc[kPartial];
     sum_records_chunked<kSumChunk>(i, P, goff, part, s_stage + (threadIdx.x >> 6) * 3 * kSumChunk, acc);
@@ -1060,6 +1076,28 @@ constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_str
 template <int MC>
 constexpr size_t multi_lds_bytes() { return sizeof(float) * multi_sh_floats<MC>(); }
 
+// The order the launch sums its views in: fixed by their cameras -- the key
+// k_sum_records stored after each view's sums (a hash of its view matrix and camera position), ties (the
+// same camera twice) in queue order -- not by the order the backward pass queued them, so a caller whose
+// threads finish their forwards in a varying order gets the same gradients bit for bit.  Position t's
+// view is bits 4t..4t+3.  Wave-uniform: nv scalar loads and scalar compares.
+static_assert(kMultiViews <= 8, "view order packed 4 bits per position");
+__device__ inline uint32_t view_order(const MultiArgs &a) {
+    typedef const __attribute__((address_space(4))) uint32_t *key_ptr;
+    uint32_t h[kMultiViews];
+#pragma unroll
+    for (int u = 0; u < kMultiViews; ++u) h[u] = u < a.nv ? ((key_ptr)a.v[u].sums)[(size_t)kPartial * a.P] : 0u;
+    uint32_t ord = 0;
+#pragma unroll
+    for (int u = 0; u < kMultiViews; ++u) {
+        int rank = 0;
+#pragma unroll
+        for (int w = 0; w < kMultiViews; ++w) rank += (w < a.nv && (h[w] < h[u] || (h[w] == h[u] && w < u))) ? 1 : 0;
+        if (u < a.nv) ord |= (uint32_t)u << (4 * rank);
+    }
+    return ord;
+}
+
 template <int MC>  // SH coefficient count (1, 4, 9, 16), or 0 without SH (colours precomputed)
 __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const MultiArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
@@ -1071,6 +1109,8 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     const bool live = i < P;
     const int ii = live ? i : i0;  // lanes past P load (and never store) row i0's parameters
     float *s_row = s_sh + threadIdx.x * RS;
+    const uint32_t ord = view_order(a);
+    auto vid = [ord](int t) { return (int)((ord >> (4 * t)) & 15u); };  // the view summed t-th
     // the Gaussian's own parameters and the first view's record sums and radius are loaded before the
     // SH row copy, so that their latency overlaps it instead of following its barrier
     const float3 mean = make_float3(a.means3D[3 * ii], a.means3D[3 * ii + 1], a.means3D[3 * ii + 2]);
@@ -1089,8 +1129,8 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     // radius are loaded one view ahead, so their latency hides behind the previous view's chains
     float nx[kPartial];
 #pragma unroll
-    for (int k = 0; k < kPartial; ++k) nx[k] = a.v[0].sums[(size_t)k * P + ii];
-    int rn = a.v[0].radii[ii];
+    for (int k = 0; k < kPartial; ++k) nx[k] = a.v[vid(0)].sums[(size_t)k * P + ii];
+    int rn = a.v[vid(0)].radii[ii];
     if constexpr (MC > 0) {  // coefficient rows, read by every view's SH chain
         sh_rows_to_lds<MC>(a.shs + (size_t)i0 * RL, nrow, s_sh);
         __syncthreads();
@@ -1105,15 +1145,16 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     bool vis = false;
     float o_act = 0.f;  // the activated opacity, from the record of a view that sees the Gaussian
     float m2[3] = {0.f, 0.f, 0.f};  // the screen-space gradient carried across views of one array
+    bool m2_have = false;            // m2 holds a value (else the next view's gradient starts it)
     const int active = (a.D + 1) * (a.D + 1);
-    for (int v = 0; v < a.nv; ++v) {
-        const MultiView &V = a.v[v];
+    for (int t = 0; t < a.nv; ++t) {
+        const MultiView &V = a.v[vid(t)];
         const int rv = rn;
         float acc[kPartial];
 #pragma unroll
         for (int k = 0; k < kPartial; ++k) acc[k] = nx[k];
-        if (v + 1 < a.nv) {
-            const MultiView &Vn = a.v[v + 1];
+        if (t + 1 < a.nv) {
+            const MultiView &Vn = a.v[vid(t + 1)];
 #pragma unroll
             for (int k = 0; k < kPartial; ++k) nx[k] = Vn.sums[(size_t)k * P + ii];
             rn = Vn.radii[ii];
@@ -1123,14 +1164,26 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         if (V.dL_dmeans2D) {
             // consecutive views writing the same array (one means2D leaf rendered from several
             // cameras) carry its value in registers: loaded at the run's first view, stored after its
-            // last -- the same additions, in view order, as a read-modify-write per view
-            const bool cont = v > 0 && a.v[v - 1].dL_dmeans2D == V.dL_dmeans2D;
-            const bool last = !(v + 1 < a.nv && a.v[v + 1].dL_dmeans2D == V.dL_dmeans2D);
+            // last -- the same additions, in view order, as a read-modify-write per view.  An array some
+            // view of the launch overwrites (a fresh .grad) starts empty at its first view in the
+            // summing order; a later run of it reloads what the earlier one stored.
+            const float *X = V.dL_dmeans2D;
+            const bool cont = t > 0 && a.v[vid(t - 1)].dL_dmeans2D == X;
+            const bool last = !(t + 1 < a.nv && a.v[vid(t + 1)].dL_dmeans2D == X);
             const float gx = r ? acc[0] : 0.f, gy = r ? acc[1] : 0.f;
-            if (!cont) old_load(V.dL_dmeans2D, 3 * (size_t)i, V.acc2, m2);
-            m2[0] = V.acc2 ? m2[0] + gx : gx;
-            m2[1] = V.acc2 ? m2[1] + gy : gy;
-            m2[2] = V.acc2 ? m2[2] + 0.f : 0.f;
+            if (!cont) {
+                bool first = true, accx = true;  // (wave-uniform scans of the launch's views)
+                for (int u = 0; u < a.nv; ++u)
+                    if (a.v[u].dL_dmeans2D == X) accx = accx && a.v[u].acc2;
+                for (int u = 0; u < t; ++u)
+                    if (a.v[vid(u)].dL_dmeans2D == X) first = false;
+                m2_have = !(first && !accx);
+                if (m2_have) old_load(V.dL_dmeans2D, 3 * (size_t)i, true, m2);
+            }
+            m2[0] = m2_have ? m2[0] + gx : gx;
+            m2[1] = m2_have ? m2[1] + gy : gy;
+            m2[2] = m2_have ? m2[2] + 0.f : 0.f;
+            m2_have = true;
             if (last) {
                 V.dL_dmeans2D[3 * i] = m2[0]; V.dL_dmeans2D[3 * i + 1] = m2[1]; V.dL_dmeans2D[3 * i + 2] = m2[2];
             }
@@ -1239,16 +1292,17 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             for (int k = 0; k < RL; ++k) s_row[k] = 0.f;
             // a view's radius, clamp mask and colour sums are loaded together (none waits for the
             // radius) and one view ahead, so the loop pays one load latency instead of two per view
-            int rv_n = a.v[0].radii[i];
-            uint8_t cm_n = a.v[0].clampm[i];
-            float g_n[3] = {a.v[0].sums[(size_t)6 * P + i], a.v[0].sums[(size_t)7 * P + i], a.v[0].sums[(size_t)8 * P + i]};
-            for (int v = 0; v < a.nv; ++v) {
-                const MultiView &V = a.v[v];
+            const MultiView &V0 = a.v[vid(0)];
+            int rv_n = V0.radii[i];
+            uint8_t cm_n = V0.clampm[i];
+            float g_n[3] = {V0.sums[(size_t)6 * P + i], V0.sums[(size_t)7 * P + i], V0.sums[(size_t)8 * P + i]};
+            for (int t = 0; t < a.nv; ++t) {
+                const MultiView &V = a.v[vid(t)];
                 const int rv = rv_n;
                 const uint8_t cm = cm_n;
                 const float g[3] = {g_n[0], g_n[1], g_n[2]};
-                if (v + 1 < a.nv) {
-                    const MultiView &Vn = a.v[v + 1];
+                if (t + 1 < a.nv) {
+                    const MultiView &Vn = a.v[vid(t + 1)];
                     rv_n = Vn.radii[i];
                     cm_n = Vn.clampm[i];
 #pragma unroll
@@ -1338,9 +1392,10 @@ static void gauss_bwd_multi_mc(const MultiArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s,
-                              const uint32_t *spec_ok) {
+                              const uint32_t *spec_ok, const float *viewmatrix, const float *campos,
+                              CamStrides cs) {
     if (P == 0) return hipSuccess;
-    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums, spec_ok);
+    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums, spec_ok, viewmatrix, campos, cs);
     return hipGetLastError();
 }
 

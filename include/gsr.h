@@ -233,7 +233,9 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
  *   gsr_backward_render     the per-pixel half of gsr_backward for one view: requests a SCRATCH
  *                           buffer through `alloc` for the view's per-(tile, Gaussian) gradient
  *                           records, then a SUMS buffer (gsr_sums_bytes(P), ABI >= 15) into which it
- *                           sums each Gaussian's records in emission order (9 x P floats, SoA).  Only
+ *                           sums each Gaussian's records in emission order (9 x P floats, SoA, then
+ *                           the view's camera key, one word: gsr_backward_gaussians sums the views in
+ *                           the order of their keys, not the order they were passed in).  Only
  *                           SUMS (and the view's GEOM, radii) must stay alive until
  *                           gsr_backward_gaussians has been queued; SCRATCH may be released once the
  *                           call returns (its last reader is queued on `stream`).
