@@ -49,8 +49,9 @@ class RenderStep:
         self.calls = 0
         # one single-thread executor per stream: a stream's views are always submitted by the same
         # thread, so the autograd nodes' sequence numbers (per-thread counters) and with them the order
-        # in which the backward visits the views -- the order the deferred multi-view pass sums them in,
-        # as AccumulateGrad would -- do not depend on which idle pool thread took which task
+        # in which the backward visits the views do not depend on which idle pool thread took which
+        # task (the deferred multi-view pass also sums a launch's views in a camera-fixed order,
+        # k_gauss_bwd_multi's view_order, so the gradients do not depend on it either)
         self.pool = ([ThreadPoolExecutor(max_workers=1) for _ in self.streams]
                      if threads and len(self.streams) > 1 else None)
 
