@@ -1016,7 +1016,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
         float *out = (float *)alloc(alloc_ctx, GSR_BUF_SUMS, gsr_sums_bytes(a.P));
         if (!out) return fail(GSR_ERR_ALLOC, "allocation callback failed (sums)");
         Phase ph(s, "sum_records");
-        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s, a.spec_ok, a.viewmatrix, a.campos, a.cs));
+        HIP_TRY(launch_sum_records(a.P, a.goff, a.part, out, s, a.spec_ok, a.viewmatrix, a.projmatrix, a.campos, a.cs, a.W, a.H));
     }
     return GSR_OK;
 }

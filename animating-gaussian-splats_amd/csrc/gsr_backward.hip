@@ -245,7 +245,8 @@ __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &an
     float alpha = CLAMP ? fminf(0.99f, o * G) : o * G;
     const bool live = j < ps.lrel;  // the entry lies before this pixel's last contributor
     if constexpr (NEAR == kNearEval) {  // the forward's near-threshold re-evaluation: the same decisions
-        const bool nr = live && near_threshold(alpha);
+        // (the forward re-evaluates only a weight it would otherwise take: p2 <= 0 included)
+        const bool nr = live && p2 <= 0.0f && near_threshold(alpha);
         if (nr) {  // (an exec-masked region, skipped when no lane has one)
             const ExactBlend e = exact_blend(a.x, a.y, rec[(size_t)kRecF4 * pl[j] + 3], o, pfx, ps.fy);
             p2 = e.power; G = e.G; alpha = e.alpha;
@@ -1030,27 +1031,35 @@ __global__ __launch_bounds__(256) void k_gauss_bwd(
 // of LDS per wave, so the walk's LDS round trips hide behind other waves; it runs on the view's
 // stream right after k_render_bwd, beside the other views' render kernels.
 constexpr int kSumChunk = 128;
-// The view's camera key (FNV-1a over the bits of its view matrix and camera position), stored after the
-// sums: k_gauss_bwd_multi orders a launch's views by it (view_order).
-__device__ inline uint32_t camera_key(const float *viewmatrix, const float *campos, CamStrides cs) {
-    float vm[16];
+// The view's camera key (FNV-1a over the bits of its view matrix, projection matrix, camera position and
+// image size), stored after the sums: k_gauss_bwd_multi orders a launch's views by it (view_order).  Two
+// views of one launch with the same key -- the same camera rendered twice, e.g. two timesteps of one
+// pose -- keep the order the backward pass queued them in (include/gsr.h, gsr_backward_gaussians).
+__device__ inline uint32_t camera_key(const float *viewmatrix, const float *projmatrix, const float *campos,
+                                      CamStrides cs, int W, int H) {
+    float vm[16], pj[16];
     load_mat16(viewmatrix, cs.v0, cs.v1, vm);
+    load_mat16(projmatrix, cs.p0, cs.p1, pj);
     const float3 cp = load_campos(campos, cs.c0);
-    const float w[19] = {vm[0], vm[1], vm[2], vm[3], vm[4], vm[5], vm[6], vm[7], vm[8], vm[9], vm[10], vm[11],
-                         vm[12], vm[13], vm[14], vm[15], cp.x, cp.y, cp.z};
     uint32_t x = 2166136261u;
+    auto mix = [&x](uint32_t w) { x = (x ^ w) * 16777619u; };
 #pragma unroll
-    for (int k = 0; k < 19; ++k) x = (x ^ __float_as_uint(w[k])) * 16777619u;
+    for (int k = 0; k < 16; ++k) mix(__float_as_uint(vm[k]));
+#pragma unroll
+    for (int k = 0; k < 16; ++k) mix(__float_as_uint(pj[k]));
+    mix(__float_as_uint(cp.x)); mix(__float_as_uint(cp.y)); mix(__float_as_uint(cp.z));
+    mix((uint32_t)W); mix((uint32_t)H);
     return x;
 }
 __global__ __launch_bounds__(256) void k_sum_records(int P, const uint32_t *__restrict__ goff,
                                                      const float4 *__restrict__ part, float *__restrict__ sums,
                                                      const uint32_t *__restrict__ spec_ok, const float *viewmatrix,
-                                                     const float *campos, CamStrides cs) {
+                                                     const float *projmatrix, const float *campos, CamStrides cs,
+                                                     int W, int H) {
     __shared__ float4 s_stage[3 * kSumChunk * 4];
     if (spec_ok && *spec_ok == 0u) return;  // (as k_render_bwd)
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        reinterpret_cast<uint32_t *>(sums)[(size_t)kPartial * P] = camera_key(viewmatrix, campos, cs);
+        reinterpret_cast<uint32_t *>(sums)[(size_t)kPartial * P] = camera_key(viewmatrix, projmatrix, campos, cs, W, H);
     const int i = blockIdx.x * 256 + threadIdx.x;
     float acc[kPartial];
     sum_records_chunked<kSumChunk>(i, P, goff, part, s_stage + (threadIdx.x >> 6) * 3 * kSumChunk, acc);
@@ -1392,10 +1401,11 @@ static void gauss_bwd_multi_mc(const MultiArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s,
-                              const uint32_t *spec_ok, const float *viewmatrix, const float *campos,
-                              CamStrides cs) {
+                              const uint32_t *spec_ok, const float *viewmatrix, const float *projmatrix,
+                              const float *campos, CamStrides cs, int W, int H) {
     if (P == 0) return hipSuccess;
-    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums, spec_ok, viewmatrix, campos, cs);
+    k_sum_records<<<div_up(P, 256), 256, 0, s>>>(P, goff, part, sums, spec_ok, viewmatrix, projmatrix, campos, cs,
+                                                 W, H);
     return hipGetLastError();
 }
 

@@ -856,7 +856,11 @@ __device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *e
     while ((int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0) {
         __builtin_amdgcn_s_sleep(100);
         if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-            if (threadIdx.x == 0) __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the gate is read again before the error is published: a gate the resolver
+            // opened during the last sleep means the redo completed first, so the outputs are final
+            if (threadIdx.x == 0 &&
+                (int32_t)(__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - seq) < 0)
+                __hip_atomic_store(err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
     }

@@ -86,8 +86,8 @@ hipError_t launch_gauss_bwd(const BwdArgs &a, hipStream_t s);
 // Each Gaussian's per-pair records of one view summed in emission order into kPartial x P SoA sums
 // (the deferred multi-view pass reads these instead of walking the records itself).
 hipError_t launch_sum_records(int P, const uint32_t *goff, const float4 *part, float *sums, hipStream_t s,
-                              const uint32_t *spec_ok, const float *viewmatrix, const float *campos,
-                              CamStrides cs);
+                              const uint32_t *spec_ok, const float *viewmatrix, const float *projmatrix,
+                              const float *campos, CamStrides cs, int W, int H);
 
 // Per-Gaussian backward over several views of the same Gaussians (gsr_backward_gaussians): one
 // launch reads the parameters and read-modify-writes every gradient once for up to kMultiViews views.

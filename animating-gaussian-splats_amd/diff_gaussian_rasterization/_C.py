@@ -898,7 +898,7 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer, 
         "seg_off": view(imgBuffer, o[12], T + 1, i32, (T + 1,)),
         "n_contrib": view(imgBuffer, o[7], W * H, i32, (H, W)),
         "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
-        "tile_flag": view(imgBuffer, o[14], T, i32, (T,)),  # 1: redone in the exact-threshold form
+        "tile_flag": view(imgBuffer, o[14], T, i32, (T,)),  # near-threshold re-evaluations (> 16: overflow tile)
         # per-pair records (index, depth bits, emission, 0) in tile-bucket order; keys = .x | .y << 32
         "pairs": view(binningBuffer, o[9], 4 * K, i32, (K, 4)),
         "keys": view(binningBuffer, o[9], 2 * K, i64, (K, 2))[:, 0],

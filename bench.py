@@ -38,9 +38,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 # rocprofv3 FETCH_SIZE / WRITE_SIZE summary of this same command (tools/profile_round.sh): HBM bytes per
 # launch of each kernel, converted per access shape (calibrated_traffic; MI355X_MICROARCH.md's 2 x
 # FETCH_SIZE + WRITE_SIZE is the streaming case and is reported beside it)
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r05_hbm_pmc.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r06_hbm_pmc.json")
 # SQ counters of the same command (tools/profile_round.sh sq passes): VALU activity per launch
-SQ_SUMMARY = os.path.join(REPO, "profiles", "r05_sq_pmc.json")
+SQ_SUMMARY = os.path.join(REPO, "profiles", "r06_sq_pmc.json")
 VALU_PEAK_GINST = 1024 * 2.4 / 2  # wave64 f32 VALU instructions per ns: 1024 SIMDs x 2.4 GHz / 2 cycles
 PHASES = ["preprocess", "bin_count", "bin_scan", "bin_emit", "tile_sort", "render_fwd", "bwd_items",
           "render_bwd", "sum_records", "gauss_bwd"]
@@ -87,6 +87,43 @@ def algorithmic_bytes(phase, P, K, N, T, F, sh):
 def pipeline_bytes(P, K, N, T, F, sh):
     """B = P (220 + 3F + 12 [SH]) + 120 K + 44 N + 16 T per fwd + bwd of one view."""
     return P * (220 + 3 * F + 12 * sh) + 120 * K + 44 * N + 16 * T
+
+
+FWD_KERNELS = ("k_preprocess", "k_bin_count", "k_bin_colscan", "k_bin_scan", "k_bin_emit", "k_tile_sort",
+               "k_chunk_sort", "k_merge_pass", "k_render_fwd")
+
+
+def step_valu(sq, views_per_gpu, median_ms, fwd_solo_ms):
+    """(valu_step, valu_render_fwd) from a tools/rocprof_summary.py `sq` summary of this command: each
+    kernel's SQ_INSTS_VALU per launch times its launches per view -- dispatches profiled over k_render_fwd's
+    for the forward kernels and over k_render_bwd's for the backward ones (the profiled bench also runs
+    forward-only probes), so k_gauss_bwd_multi counts 1/V; without dispatch counts one per view and
+    k_gauss_bwd_multi one per step -- summed over the step's views, over the median step at the VALU
+    issue peak."""
+    fwd, bwd = sq.get("k_render_fwd"), sq.get("k_render_bwd")
+    if not fwd or not bwd or "SQ_INSTS_VALU" not in fwd:
+        return None, None
+    per_view, kernels = 0.0, {}
+    for k, v in sq.items():
+        if "SQ_INSTS_VALU" not in v:
+            continue
+        ref = fwd if k in FWD_KERNELS else bwd
+        if v.get("launches") and ref.get("launches"):
+            lpv = v["launches"] / ref["launches"]
+        else:
+            lpv = 1.0 / views_per_gpu if k == "k_gauss_bwd_multi" else 1.0
+        per_view += v["SQ_INSTS_VALU"] * lpv
+        kernels[k] = round(v["SQ_INSTS_VALU"] * lpv / 1e6, 2)
+    insts = per_view * views_per_gpu
+    step = {"insts_per_step": int(insts), "peak_Ginst_s": VALU_PEAK_GINST,
+            "issue_frac": round(insts / (VALU_PEAK_GINST * 1e9 * median_ms * 1e-3), 4),
+            "M_insts_per_view_by_kernel": kernels, "source": os.path.relpath(SQ_SUMMARY, REPO)}
+    f = None
+    if fwd_solo_ms:
+        f = {"insts_per_launch": int(fwd["SQ_INSTS_VALU"]), "solo_ms": round(fwd_solo_ms, 5),
+             "issue_frac": round(fwd["SQ_INSTS_VALU"] / (VALU_PEAK_GINST * 1e9 * fwd_solo_ms * 1e-3), 4),
+             "salu_per_valu": round(fwd.get("SQ_INSTS_SALU", 0) / fwd["SQ_INSTS_VALU"], 3)}
+    return step, f
 
 
 def cpu_baseline_oracle(cfg, params_cpu, cam_cpu, dl_cpu, threads=0):
@@ -1112,6 +1149,11 @@ def main():
                 pk = 1024 * q["clock_ghz"] / 2  # Ginst/s at that clock
                 valu["profile_clock_ghz"] = round(q["clock_ghz"], 3)
                 valu["issue_frac_at_profile_clock"] = round(rate / pk, 4)
+    valu_step = valu_fwd = None
+    if os.path.exists(SQ_SUMMARY) and args.config == "C3" and args.step_shape == "summed":
+        valu_step, valu_fwd = step_valu(json.load(open(SQ_SUMMARY)), views_per_step / world, median_ms,
+                                        solo["render_fwd"][0] / solo["render_fwd"][1]
+                                        if solo and solo["render_fwd"][1] else None)
     bytes_launch = algorithmic_bytes(dom, cfg.P, K, N, T, F, SH)
     # the roofline uses the kernel's own duration: the solo probe (one stream, nothing else on the chip)
     # when there is one; the in-step event interval (which overlaps the other streams' kernels) is
@@ -1197,6 +1239,11 @@ def main():
                          "binding_resource": "VALU issue (blend evaluations: ~256 pixel-Gaussian pairs per "
                                              "pair record); HBM traffic is a small share of the kernel time",
                          "valu": valu,
+                         # the step's binding resource: every library kernel's wave64
+                         # VALU instructions per step (profiled per launch) over the median step time, against
+                         # one instruction per 2 cycles on every SIMD at 2.4 GHz
+                         "valu_step": valu_step,
+                         "valu_render_fwd": valu_fwd,
                          "pipeline": {"bytes_per_view": int(pipe_b),
                                       "formula": "P*(220 + 3F + 12*SH) + 120*K + 44*N + 16*T (SURVEY.md 8(d))",
                                       "achieved_GBps_per_gpu": round(pipe_gbps, 1),

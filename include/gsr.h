@@ -234,8 +234,11 @@ int gsr_backward(const gsr_camera *cam, const gsr_gaussians *g, const int *radii
  *                           buffer through `alloc` for the view's per-(tile, Gaussian) gradient
  *                           records, then a SUMS buffer (gsr_sums_bytes(P), ABI >= 15) into which it
  *                           sums each Gaussian's records in emission order (9 x P floats, SoA, then
- *                           the view's camera key, one word: gsr_backward_gaussians sums the views in
- *                           the order of their keys, not the order they were passed in).  Only
+ *                           the view's camera key, one word -- a hash of its view and projection
+ *                           matrices, camera position and image size: gsr_backward_gaussians sums the
+ *                           views in the order of their keys, not the order they were passed in;
+ *                           views with equal keys, i.e. the same camera passed twice in one launch,
+ *                           keep the order they were passed in, so their sum depends on it).  Only
  *                           SUMS (and the view's GEOM, radii) must stay alive until
  *                           gsr_backward_gaussians has been queued; SCRATCH may be released once the
  *                           call returns (its last reader is queued on `stream`).
@@ -325,8 +328,10 @@ size_t gsr_spec_binning_bytes(int P, int width, int height, int prepare_backward
  * n_contrib, tile_maxc}, binning {pairs (16-byte records: index, depth bits, emission, 0),
  * point_list, slot_emit}, image {seg_off}, binning {seg_state (the blend state at every interior
  * 128-entry boundary of every tile list: 256 float4 (C0, C1, C2, T) per boundary)}, image
- * {tile_flag (ABI 21: per tile, 1 when the forward redid it in the exact-threshold form)}.  Returns
- * the count written (15, or max_out if smaller). */
+ * {tile_flag (ABI 21: per tile, the count of near-threshold weights the forward re-evaluated inline in
+ * the exact-threshold form; their records follow in IMAGE near_rec, at most 16 per tile, and a count
+ * above 16 sends the tile's backward items to the re-evaluating k_render_bwd<true>)}.  Returns the count
+ * written (15, or max_out if smaller). */
 int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *out, int max_out);
 
 const char *gsr_last_error(void);
@@ -336,10 +341,12 @@ int gsr_abi_version(void);
  * load turns it off).  The render kernels evaluate the blend weight as 2^(power log2 e) with FMAs and
  * the hardware exp, which differs from the reference's expf(power) (renderCUDA, forward.cu /
  * backward.cu) by a few ulp; a (pixel, Gaussian) weight that close to 1/255 can take the other side of
- * the threshold.  With the mode on, k_render_fwd's fast pass notes whether any weight it took lies
- * within 1e-5 (relative) of 1/255; such a tile (a few % of them) is redone at once with those weights
- * re-evaluated in the reference's expression order and a double-precision exp, and its backward items
- * run the same re-evaluation (IMAGE tile_flag), so decisions match the reference's.
+ * the threshold.  With the mode on, k_render_fwd re-evaluates every weight it would take that lies
+ * within 1e-5 (relative) of 1/255 inline, in the reference's expression order with a double-precision
+ * exp, and appends (list position, pixel, power, G, alpha) to the tile's near records (IMAGE near_rec,
+ * 16 per tile; IMAGE tile_flag = the tile's count).  The backward's walk looks those weights up in the
+ * records; a tile with more than 16 re-evaluates them itself (k_render_bwd<true>).  So decisions match
+ * the reference's.
  * The backward follows the flags its forward wrote, so the setting may change at any time; it applies
  * to forwards queued after the call.  Returns the previous setting. */
 int gsr_set_exact_thresholds(int on);

@@ -535,11 +535,14 @@ def test_exact_tiles_flagged_and_redone(cuda):
     check_backward(gb, gref, P, st["M"], allow("c1")[1])
 
 
-def test_near_record_overflow(cuda):
+@pytest.mark.parametrize("where", ["band", "centre"])
+def test_near_record_overflow(where, cuda):
     """40 copies of one Gaussian whose weight at one pixel sits on 1/255 (opacity solved from the
     oracle's power there): 40 near-threshold re-evaluations in one tile, more than the kNearCap = 16
     records the backward can look up, so that tile's items take the re-evaluating backward kernel.
-    Forward and gradients against the oracle with no allowance."""
+    `band`: a pixel whose power is about -1.5; `centre`: the pixel nearest the Gaussian's
+    centre, power near 0 and opacity near 1/255, where the fast power's sign test and the exact one
+    meet.  Forward and gradients against the oracle with no allowance."""
     W, H = 64, 48
     base, rs = _inputs(300, W, H, 64.0, 0.05, seed=5)
     st0 = _ora_forward(base, rs)
@@ -554,7 +557,10 @@ def test_near_record_overflow(cuda):
         for px in range(max(0, int(gx_) - 6), min(W, int(gx_) + 7)):
             dx, dy = np.float32(gx_ - np.float32(px)), np.float32(gy_ - np.float32(py))
             pw = np.float32(np.float32(-0.5) * (A * dx * dx + C * dy * dy) - B * dx * dy)
-            if -3.0 < pw < -0.5 and (best is None or abs(pw + 1.5) < abs(best[2] + 1.5)):
+            if where == "band":
+                if -3.0 < pw < -0.5 and (best is None or abs(pw + 1.5) < abs(best[2] + 1.5)):
+                    best = (px, py, pw)
+            elif pw <= 0.0 and (best is None or abs(pw) < abs(best[2])):
                 best = (px, py, pw)
     assert best is not None
     px, py, pw = best

@@ -44,3 +44,26 @@ def test_lint_flags_the_round3_defect(tmp_path):
                    cwd=src, check=True, capture_output=True)
     bad = lds_lint.lint_library(str(so))
     assert any("k_render_fwd" in b for b in bad), bad
+
+
+# ---- DPP data hazards (tools/dpp_hazard_lint.py) ---------------------------------------
+import dpp_hazard_lint  # noqa: E402
+import dpp_hazard_variant  # noqa: E402
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libgsr.so not built")
+def test_shipped_library_has_no_dpp_hazard():
+    """Every DPP instruction of the shipped code object -- the compiler's and row_halves3's inline
+    v_add_f32_dpp stages -- reads VGPRs written at least 2 wait states earlier on every path."""
+    assert dpp_hazard_lint.dpp_count(LIB) > 100
+    assert dpp_hazard_lint.lint_library(LIB) == []
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_dpp_lint_flags_the_round5_defect(tmp_path):
+    """The pair reduction with one asm statement per DPP stage and no s_nop (the round-5 work-in-progress
+    form) must be flagged at k_render_bwd."""
+    so = tmp_path / "dpphaz.so"
+    dpp_hazard_variant.make_variant(str(so), sources=["gsr_backward.hip"])
+    bad = dpp_hazard_lint.lint_library(str(so))
+    assert any("k_render_bwd" in b and "v_add_f32_dpp" in b for b in bad), bad

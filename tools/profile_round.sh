@@ -25,7 +25,7 @@ echo "write ok"
 for pass in 1 2; do
   if [ $pass = 1 ]; then CTR="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE";
   else CTR="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC SQ_WAIT_ANY SQ_INSTS_VALU_TRANS_F32"; fi
-  timeout -k 10 400 rocprofv3 --pmc $CTR --kernel-include-regex "render|gauss_bwd|preprocess|bin_emit" --kernel-trace --output-format csv -d "$O/sq$pass" -- \
+  timeout -k 10 400 rocprofv3 --pmc $CTR --kernel-include-regex "gsr::" --kernel-trace --output-format csv -d "$O/sq$pass" -- \
       python3 "$R/bench.py" --no-cpu-baseline $BENCH_LEGS "$@" > "$O/sq$pass.log" 2>&1 || { echo "sq pass $pass failed rc=$?"; exit 4; }
 done
 echo "sq ok"

@@ -95,6 +95,8 @@ def sq(dirs):
     out = {}
     for k, v in acc.items():
         o = {c: sum(x) / len(x) for c, x in v.items()}
+        if "SQ_INSTS_VALU" in v:  # dispatches profiled (bench.py: launches per view -> VALU per step)
+            o["launches"] = len(v["SQ_INSTS_VALU"])
         if dur.get(k):
             o["avg_us_in_pass"] = sum(dur[k]) / len(dur[k])
             if "GRBM_GUI_ACTIVE" in o:  # summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)
