@@ -205,6 +205,12 @@ std::atomic<int> g_exact{[] {
     return (e && e[0] == '0') ? 0 : 1;
 }()};
 
+// k_render_bwd's 8x8-quarter layout (round 6 structural A/B): GSR_BWD_Q8=1 at load
+const int g_bwd_q8 = [] {
+    const char *e = getenv("GSR_BWD_Q8");
+    return (e && e[0] == '1') ? 1 : 0;
+}();
+
 void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
     memset(&a, 0, sizeof(a));
     a.exact = g_exact.load(std::memory_order_relaxed);
@@ -245,6 +251,7 @@ void carve_image(FwdArgs &a, char *base) {
     a.items_ws = (uint32_t *)(base + L.items_ws);
     a.scan_ws = (uint32_t *)(base + L.scan_ws); a.tile_rank = (uint32_t *)(base + L.tile_rank);
     a.tile_flag = (uint32_t *)(base + L.tile_flag); a.near_rec = (float4 *)(base + L.near_rec);
+    a.tsat_list = (uint32_t *)(base + L.tsat_list);
 }
 void carve_binning(FwdArgs &a, char *base, int K) {
     const BinningLayout L(K, a.P);
@@ -986,6 +993,7 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     memset(&a, 0, sizeof(a));
     a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
     a.act = f.act;
+    a.q8 = g_bwd_q8;
     a.scale_modifier = f.scale_modifier; a.tan_fovx = f.tan_fovx; a.tan_fovy = f.tan_fovy;
     a.focal_x = f.focal_x; a.focal_y = f.focal_y;
     a.means3D = f.means3D; a.scales = f.scales; a.rotations = f.rotations; a.shs = f.shs;

@@ -128,6 +128,9 @@ constexpr int kOrderBuckets = 2048;
 // counter [2 kOrderBuckets].  k_bin_count zeroes it in every forward; the count kernel's last block
 // leaves the counts and the counter at zero again, so a second build (a repeated backward) starts clean.
 constexpr int kItemsWsWords = 2 * kOrderBuckets + 64;
+// items_ws word counting the pixels the exact saturation re-walk redoes (zeroed with the workspace by
+// k_bin_count; the item kernels use words [0, 2 kOrderBuckets])
+constexpr int kTSatCtr = 2 * kOrderBuckets + 8;
 
 // The single-pass tile scan of k_bin_colscan (IMAGE.scan_ws, zeroed by k_bin_count): one look-back
 // word per block of tiles (u64: flag in bits 62-63 -- kScanAgg: the block's own sums, kScanInc: the sums
@@ -158,7 +161,8 @@ __host__ __device__ inline uint32_t lpt_bucket(uint32_t c) {
 constexpr uint32_t kNearCap = 16;
 struct ImageLayout {
     size_t ranges, pix_end, n_contrib, tile_maxc, tile_order_f, seg_off, sort_lists,
-        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, scan_ws, tile_rank, tile_flag, near_rec, chunk_off, total;
+        tile_count, tile_cursor, block_sums, block_off, meta, items_ws, scan_ws, tile_rank, tile_flag, tsat_list,
+        near_rec, chunk_off, total;
     __host__ __device__ ImageLayout(int W, int H, int P) {
         const int T = div_up(W, kTileW) * div_up(H, kTileH);
         const int N = W * H;
@@ -167,7 +171,7 @@ struct ImageLayout {
         ranges = o;      o = align256(o + sizeof(uint2) * T);
         pix_end = o;     o = align256(o + sizeof(float4) * N);
         n_contrib = o;   o = align256(o + sizeof(uint32_t) * N);
-        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter tile (16x4 px)
+        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 8 * T);  // per 16x4 strip, then per 8x8 quarter
         tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
         seg_off = o;     o = align256(o + sizeof(uint32_t) * (T + 1));
         sort_lists = o;  o = align256(o + sizeof(uint32_t) * T);      // tiles longer than kFwdSortCap
@@ -180,6 +184,7 @@ struct ImageLayout {
         scan_ws = o;     o = align256(o + sizeof(uint32_t) * kScanWsWords);
         tile_rank = o;   o = align256(o + sizeof(uint32_t) * T);           // rank inside its LPT bucket
         tile_flag = o;   o = align256(o + sizeof(uint32_t) * T);           // near-threshold re-evaluations
+        tsat_list = o;   o = align256(o + sizeof(uint32_t) * N);           // pixels the exact re-walk redoes
         near_rec = o;    o = align256(o + sizeof(float4) * kNearCap * T);  // and their records
         // (chunk, tile) counts, then each chunk's slab offset inside the tile's range (LDS binning)
         chunk_off = o;   o = align256(o + (T <= kMaxLdsTiles ? sizeof(uint32_t) * (size_t)NB * T : 0));
@@ -614,6 +619,18 @@ __device__ inline bool blend_ok(const Blend &e) { return e.p2 <= 0.0f && e.alpha
 constexpr float kNearRel = 1e-5f;
 constexpr float kNearLo = (1.0f / 255.0f) * (1.0f - kNearRel), kNearHi = (1.0f / 255.0f) * (1.0f + kNearRel);
 __device__ inline bool near_threshold(float alpha) { return alpha >= kNearLo && alpha < kNearHi; }
+// The same for the transmittance test T (1 - alpha) >= 1e-4 (round 6).  The fast
+// forward's T (one fmaf per contributor, v_exp_f32 weights) drifts from the reference's (two roundings
+// per contributor, the exact weights) by at most t_window(L) relative after L list entries: <= 3
+// roundings of 2^-24 per contributor (kTW1) plus the weights' few-ulp differences, which T accumulates
+// as sum alpha / (1 - alpha) * (their relative error) <= 5e-5 (kTW0) for T >= 1e-4 -- measured at most
+// 4.7e-6 over C2 / C3 / C4 views (tools/t_drift.py).  In the exact-threshold mode the fast
+// walk goes on while test_T >= 1e-4 (1 - t_window), so it never stops before the reference would, and
+// every pixel whose final T is below 1e-4 (1 + t_window(n_contrib)) -- the only ones whose stop can
+// differ -- is redone by k_render_tsat, the reference's walk for that pixel with the exact weights.
+constexpr float kTSat = 1e-4f;
+constexpr float kTW0 = 5e-5f, kTW1 = 2e-7f;
+__device__ inline float t_window(uint32_t L) { return kTW0 + kTW1 * (float)L; }
 // exact (power, G, alpha) of the Gaussian at (gx, gy) with exact conic (ca, cb, cc) and opacity o.  Not
 // inlined (the double-precision exp would hold registers in the hot loops) and returned by value (a
 // by-reference output would put the caller's blend variables in scratch memory).

@@ -878,7 +878,8 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, uint32_t *__restrict__ tile_maxc,
     const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok,
     int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err, uint64_t gate_timeout,
-    uint32_t *__restrict__ tile_flag, float4 *__restrict__ near_rec) {
+    uint32_t *__restrict__ tile_flag, float4 *__restrict__ near_rec, uint32_t *__restrict__ tsat_n,
+    uint32_t *__restrict__ tsat_list) {
     __shared__ uint64_t s_key[sort_slots(kFwdSortCap)];
     __shared__ union {
         uint32_t val[sort_slots(kFwdSortCap)];  // sort payload (emission index), until written out
@@ -1000,12 +1001,16 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
         if (!((live >> wv) & 1u)) m = 0;
         // batch-uniform: some staged entry's opacity exceeds 0.99 (the backward takes the same variant)
         const bool clamp = __builtin_amdgcn_ballot_w64((qw & 16u) != 0u) != 0;
+        // the transmittance test's bound for this batch's entries (EXACT: widened by the drift window at
+        // the batch's last position, gsr_common.h t_window)
+        const float t_stop = EXACT ? kTSat * (1.0f - t_window((uint32_t)base + 64u)) : kTSat;
         // one entry's blend into this pixel's state (front to back)
         auto take = [&](const Blend &e, bool ok, float4 b, float4 c, int j) {
             const float test_T = fmaf(-e.alpha, Tt, Tt);  // T (1 - alpha), one rounding
             // keep == !(test_T < 1e-4) (test_T is never NaN: T in (0, 1], alpha in [0, 0.99]); the
-            // pixel finishes when it takes the entry but may not keep it
-            const bool use = ok && test_T >= 0.0001f;
+            // pixel finishes when it takes the entry but may not keep it.  EXACT: on while test_T >=
+            // 1e-4 (1 - t_window) (this batch's bound), the pixels that end near 1e-4 are redone by k_render_tsat
+            const bool use = ok && test_T >= t_stop;
             thr = (ok && !use) ? kThrDone : thr;
             if (use) {  // an exec-masked update: no selects for w, T and the last contributor (-1 %)
                 const float w = e.alpha * Tt;
@@ -1048,6 +1053,8 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     }
     if (inside) {
         const int pid = py * W + px;
+        if (EXACT && Tt < kTSat * (1.0f + t_window(last)))  // (rare: k_render_tsat redoes the pixel)
+            tsat_list[atomicAdd(tsat_n, 1u)] = (uint32_t)pid;
         pix_end[pid] = make_float4(C01.x, C01.y, C2D.x, Tt);
         n_contrib[pid] = last;
         out_color[pid] = C01.x + Tt * bg[0];
@@ -1060,6 +1067,9 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     uint32_t mx = last;
 #pragma unroll
     for (int d = 16; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));  // within 32 lanes
+    // and the 8x8 quarter's (this wave's) maximum, after the T strips' (the Q8 backward layout)
+    const uint32_t mq8 = max(mx, (uint32_t)__shfl_xor((int)mx, 32, 64));
+    if (lane == 0) tile_maxc[4 * T + 4 * tile + wv] = mq8;
     __syncthreads();  // every wave is past its last read of s_u
     if (threadIdx.x < 4) s_u.st.q[threadIdx.x] = 0;
     __syncthreads();
@@ -1071,6 +1081,109 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
 #endif
+}
+
+// Exact saturation re-walk (exact-threshold mode; round 6).  One wave per pixel
+// k_render_fwd flagged (final T below 1e-4 (1 + t_window(n_contrib)), gsr_common.h): the reference's
+// front-to-back walk (SURVEY.md 2.1 row renderCUDA fwd, oracle/gsr_oracle.c ora_render) for that one
+// pixel.  The lanes evaluate 64 list entries at a time -- the fast weight decides which can contribute,
+// as in k_render_fwd (p2 <= 0, alpha >= kNearLo; a weight in the near window is decided by its exact
+// value), and every contributor's weight is the exact one, min(0.99, o exp(power)) with the reference's
+// expression order and a double-precision exp -- then the wave applies them in list order with the
+// reference's operations: test_T = T * (1 - alpha), stop below 1e-4, C += c * alpha * T.  So n_contrib,
+// T and the blended colour / depth are the reference's.  The pixel's outputs, its end state for the
+// backward and its state at every segment boundary of the tile's list are rewritten.  The walk can only
+// end earlier than the fast one did (t_stop in k_render_fwd), so only the entries before the fast
+// n_contrib are evaluated, the tile's quarter maxima stay upper bounds, and every entry it takes was
+// seen by the fast walk (whose near records the backward looks up).  Latency-bound by design (a few
+// thousand pixels per 1080p view): the render records of the next 64 entries are in flight while the
+// current ones are applied, and the grid has a wave for every flagged pixel up to kTSatBlocks.
+constexpr int kTSatBlocks = 4096;
+struct TSatRec { float4 r0, r1, r2, r3; };
+__device__ inline TSatRec tsat_load(const float4 *__restrict__ rec, uint32_t g, bool v) {
+    TSatRec t;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 *r = rec + (size_t)kRecF4 * g;
+    t.r0 = v ? r[0] : z; t.r1 = v ? r[1] : z; t.r2 = v ? r[2] : z; t.r3 = v ? r[3] : z;
+    return t;
+}
+__global__ __launch_bounds__(64) void k_render_tsat(
+    int W, int gx, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list,
+    const float4 *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
+    float *__restrict__ out_depth, float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib,
+    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ tsat_n,
+    const uint32_t *__restrict__ tsat_list, const uint32_t *__restrict__ spec_ok, int ks, int HW) {
+    if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
+    const uint32_t cnt = *tsat_n;
+    const int lane = threadIdx.x;
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const uint32_t pid = tsat_list[i];
+        const int px = (int)(pid % (uint32_t)W), py = (int)(pid / (uint32_t)W);
+        const int tile = (py / kTileH) * gx + px / kTileW;
+        const uint2 rg = ranges[tile];
+        const int n = (int)(rg.y - rg.x);
+        const int nf = (int)n_contrib[pid];  // the fast walk's: the exact one ends at or before it
+        const float pfx = (float)px, pfy = (float)py;
+        const int lx = px % kTileW, ly = py % kTileH;
+        const int bslot = 64 * (ly >> 2) + 16 * (ly & 3) + lx;  // the backward's pixel slot (k_render_fwd)
+        const size_t sb = seg_off[tile];
+        float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
+        uint32_t last = 0;
+        bool done = false;
+        // entries base + lane: point list two groups ahead, render records one group ahead
+        uint32_t g_next = lane < nf ? point_list[rg.x + lane] : 0u;
+        TSatRec cur = tsat_load(rec, g_next, lane < nf);
+        g_next = 64 + lane < nf ? point_list[rg.x + 64 + lane] : 0u;
+        for (int base = 0; base < n; base += 64) {
+            // the state in front of entry `base` at a segment boundary (past the stop: the final state)
+            if (base > 0 && (base & ((1 << ks) - 1)) == 0 && lane == 0)
+                seg_state[(sb + ((uint32_t)base >> ks) - 1u) * kTilePix + bslot] = make_float4(C0, C1, C2, T);
+            if (done || base >= nf) continue;
+            const int e = base + lane;
+            const TSatRec t = cur;
+            cur = tsat_load(rec, g_next, e + 64 < nf);
+            g_next = e + 128 < nf ? point_list[rg.x + e + 128] : 0u;
+            bool take = false;
+            float al = 0.f;
+            if (e < nf) {
+                const Blend eb = blend_eval<true>(t.r0, t.r1, pfx, pfy);
+                if (eb.p2 <= 0.0f && eb.alpha >= kNearLo) {  // k_render_fwd's live test (exact mode)
+                    const ExactBlend x = exact_blend(t.r0.x, t.r0.y, t.r3, t.r1.y, pfx, pfy);
+                    take = eb.alpha >= kNearHi || (x.power <= 0.0f && x.alpha >= 1.0f / 255.0f);
+                    al = x.alpha;
+                }
+            }
+            uint64_t m = __ballot(take);
+            while (m) {  // wave-uniform: the reference's serial update, entry by entry
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al), j));
+                const float test_T = T * (1.0f - a);
+                if (test_T < kTSat) {
+                    done = true;
+                    break;
+                }
+                const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.x), j));
+                const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.y), j));
+                const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.z), j));
+                const float cd = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.w), j));
+                C0 += cx * a * T;
+                C1 += cy * a * T;
+                C2 += cz * a * T;
+                D += cd * a * T;
+                T = test_T;
+                last = (uint32_t)(base + j + 1);
+            }
+        }
+        if (lane == 0) {
+            pix_end[pid] = make_float4(C0, C1, C2, T);
+            n_contrib[pid] = last;
+            out_color[pid] = C0 + T * bg[0];
+            out_color[HW + pid] = C1 + T * bg[1];
+            out_color[2 * HW + pid] = C2 + T * bg[2];
+            out_depth[pid] = D;
+        }
+    }
 }
 
 __global__ void k_zero_f32(float *p, size_t n) {
@@ -1191,7 +1304,12 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     k<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                         a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
                         a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
-                        a.gate_err, a.gate_timeout, a.tile_flag, a.near_rec);
+                        a.gate_err, a.gate_timeout, a.tile_flag, a.near_rec, a.items_ws + kTSatCtr, a.tsat_list);
+    if (a.exact)  // the flagged pixels' exact re-walk (a fixed grid that loops over the device-side count)
+        k_render_tsat<<<kTSatBlocks, 64, 0, s>>>(a.W, a.gx, a.ranges, a.point_list, a.rec, a.bg, a.out_color,
+                                                 a.out_depth, a.pix_end, a.n_contrib, a.seg_off, a.seg_state,
+                                                 a.items_ws + kTSatCtr, a.tsat_list, a.spec_ok, seg_log2(a.P),
+                                                 a.W * a.H);
     return hipGetLastError();
 }
 

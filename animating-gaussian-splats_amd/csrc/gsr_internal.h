@@ -22,6 +22,9 @@ struct FwdArgs {
     // exact-threshold mode: per tile, the count of near-threshold weights k_render_fwd re-evaluated, and
     // their records (kNearCap per tile: key (list position << 8 | pixel), power, G, alpha)
     uint32_t *tile_flag; float4 *near_rec;
+    // exact-threshold mode: pixels whose final T lies within t_window of 1e-4, redone by k_render_tsat
+    // (count in items_ws[kTSatCtr])
+    uint32_t *tsat_list;
     // binning
     uint4 *pairs; uint32_t *point_list; uint32_t *slot_emit; float4 *seg_state;
     // outputs
@@ -44,6 +47,7 @@ constexpr int kSpecSortBlocks = 512;
 
 struct BwdArgs {
     int P, D, M, W, H, gx, gy, K, act;
+    int q8;  // k_render_bwd's 8x8-quarter layout (GSR_BWD_Q8=1; round 6 structural variant)
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *means3D, *scales, *rotations, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;

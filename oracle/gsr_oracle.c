@@ -275,6 +275,13 @@ long ora_bin(int P, const float *depths, const int *radii, const int *rects,
     return K;
 }
 
+/* The blend weight's exponential.  The reference's renderCUDA calls CUDA's single-precision exp (a few
+ * ulp, not correctly rounded; no CUDA here), glibc's expf is not correctly rounded either (<= 0.502
+ * ulp), so neither gives the reference's bits.  The restatement uses the correctly rounded value -- the
+ * double-precision exp rounded to float -- a definition independent of the libm at hand, which the GPU's
+ * exact-threshold evaluations (gsr_common.h exact_blend, k_render_tsat) reproduce bit for bit. */
+static inline float ora_expf(float x) { return (float)exp((double)x); }
+
 /* ======================================================================================
  * Forward: front-to-back alpha blend of colour and depth (SURVEY 2.1 row renderCUDA fwd)
  * ====================================================================================== */
@@ -299,7 +306,7 @@ void ora_render(const unsigned *ranges, const unsigned *point_list, int W, int H
                         const float *co = conic_opacity + 4 * g;
                         const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                         if (power > 0.0f) continue;
-                        const float alpha = fminf(0.99f, co[3] * expf(power));
+                        const float alpha = fminf(0.99f, co[3] * ora_expf(power));
                         if (alpha < 1.0f / 255.0f) continue;
                         const float test_T = T * (1 - alpha);
                         if (test_T < 0.0001f) break;
@@ -368,7 +375,7 @@ void ora_render_backward(const unsigned *ranges, const unsigned *point_list, int
                         const float *co = conic_opacity + 4 * g;
                         const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                         if (power > 0.0f) continue;
-                        const float G = expf(power);
+                        const float G = ora_expf(power);
                         const float alpha = fminf(0.99f, co[3] * G);
                         if (alpha < 1.0f / 255.0f) continue;
                         trans = trans / (1.f - alpha);

@@ -33,7 +33,10 @@ pytestmark = pytest.mark.gpu
 # 1.29e-6 / 6.0e-6)
 ALLOW = {
     "C3_summed": dict(pix=0.0, grad=0.0),         # measured 0 / 0
-    "C5_view": dict(pix=1.93e-6, grad=1.4e-5),    # measured 4.8e-7 / 3.5e-6
+    # C5 activates its inputs on the GPU (rasterize_parameters' fused activations) and the oracle gets torch's
+    # CPU activations: ulp-level input differences, not the rasterizer's decisions (measured round 6: one
+    # pixel of 6.2M, 1.6e-7; round 5 with the saturation flips: 4.8e-7 / 3.5e-6)
+    "C5_view": dict(pix=1e-6, grad=1.4e-5),
 }
 VIEWS = [0, 1, 2, 3, 4]  # the bench's first step: rig cameras 0-4 (height -0.8, yaw 0..160)
 
