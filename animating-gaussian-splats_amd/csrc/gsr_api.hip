@@ -205,12 +205,6 @@ std::atomic<int> g_exact{[] {
     return (e && e[0] == '0') ? 0 : 1;
 }()};
 
-// k_render_bwd's 8x8-quarter layout (round 6 structural A/B): GSR_BWD_Q8=1 at load
-const int g_bwd_q8 = [] {
-    const char *e = getenv("GSR_BWD_Q8");
-    return (e && e[0] == '1') ? 1 : 0;
-}();
-
 void fill_common(FwdArgs &a, const gsr_camera *cam, const gsr_gaussians *g) {
     memset(&a, 0, sizeof(a));
     a.exact = g_exact.load(std::memory_order_relaxed);
@@ -296,11 +290,12 @@ int gsr_buffer_offsets(int P, int W, int H, int K, size_t *out, int max_out) {
     const GeomLayout g(P);
     const ImageLayout im(W, H, P);
     const BinningLayout b(K, P);
-    const size_t v[15] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
+    const size_t v[16] = {g.depth, g.rec, g.rect, g.tiles, g.goff,
                           im.ranges, im.pix_end, im.n_contrib, im.tile_maxc,
-                          b.pairs, b.point_list, b.slot_emit, im.seg_off, b.seg_state, im.tile_flag};
+                          b.pairs, b.point_list, b.slot_emit, im.seg_off, b.seg_state, im.tile_flag,
+                          im.items_ws + sizeof(uint32_t) * kTSatCtr};
     int n = 0;
-    for (; n < 15 && n < max_out; ++n) out[n] = v[n];
+    for (; n < 16 && n < max_out; ++n) out[n] = v[n];
     return n;
 }
 
@@ -993,7 +988,6 @@ int backward_render(const gsr_camera *cam, const gsr_gaussians *g, const int *ra
     memset(&a, 0, sizeof(a));
     a.P = f.P; a.D = f.D; a.M = f.M; a.W = f.W; a.H = f.H; a.gx = f.gx; a.gy = f.gy; a.K = num_rendered;
     a.act = f.act;
-    a.q8 = g_bwd_q8;
     a.scale_modifier = f.scale_modifier; a.tan_fovx = f.tan_fovx; a.tan_fovy = f.tan_fovy;
     a.focal_x = f.focal_x; a.focal_y = f.focal_y;
     a.means3D = f.means3D; a.scales = f.scales; a.rotations = f.rotations; a.shs = f.shs;

@@ -169,7 +169,7 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
 // tail inputs live in a register pair that the compiler parks in scratch during the walk: one store and
 // one load per batch).  1 % faster alone than 6 waves (profiles/r05_bwd_waves_ab.txt; 5 -> 6 was 3 %).
 // The near-overflow variant keeps 4 (its re-evaluation call site needs the registers).
-#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 4 : (Q8 ? 6 : 7), 8)))
+#define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 4 : 7, 8)))
 constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
 constexpr int kExactBwdBlocks = 256;  // grid of the exact-threshold tiles' k_render_bwd
 
@@ -217,42 +217,10 @@ __device__ inline PairSums pair_sums(float S0, float S1, float S4, float cs0, fl
     return r;
 }
 
-// The same for the 8x8-quarter layout (Q8, round 6 structural variant): lane l holds
-// column cx = l & 7 and row ry = l >> 3 of each 8x8 quarter, so its 4 pixels lie in two columns, A (the
-// even quarters, offset dxA) and B = A + 8 (the odd quarters, dxB = dxA - 8).  The lane keeps the B
-// pixels' S0 and S1 apart too (S0B, S1B), so the column weights stay one per lane: sum dx S0 =
-// dxA S0 - 8 S0B, sum dx^2 S0 = dxA (dxA S0 - 8 S0B) - 8 dxB S0B, sum dx S1 = dxA S1 - 8 S1B.  Rows are
-// folded over ry (permlane32, permlane16, then DPP row_ror:8), the weights applied per column, and the 8
-// columns of each row summed by 2 DPP stages into the same parity halves and slots as pair_sums.
-__device__ inline void row_halves3_q8(float &X, float &Y, float &Z) {
-    asm("s_nop 1\n\t"
-        "v_add_f32_dpp %0, %0, %0 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_add_f32_dpp %1, %1, %1 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_add_f32_dpp %2, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_add_f32_dpp %0, %0, %0 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_add_f32_dpp %1, %1, %1 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_add_f32_dpp %2, %2, %2 row_ror:2 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-        : "+v"(X), "+v"(Y), "+v"(Z));
-}
-__device__ inline float ror8_add(float v) {  // v + v of the lane 8 further in the 16-lane row
-    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
-}
-__device__ inline PairSums pair_sums_q8(float S0, float S1, float S4, float S0B, float S1B, float cs0, float cs1,
-                                        float cs2, float dxA, const RowW &w) {
-    const float pA = fold32(S0, S1), pB = fold32(S4, cs0), pC = fold32(S0B, S1B), pD = fold32(cs1, cs2);
-    const float rA = ror8_add(fold16(pA, pB));  // column sums, rows [S0, S4, S1, cs0]
-    const float rC = ror8_add(fold16(pC, pD));  // rows [S0B, cs1, S1B, cs2]
-    const float xs = fmaf(dxA, rA, -8.f * rC);                  // rows 0 / 2: sum dx S0 / sum dx S1
-    const float ys = fmaf(dxA, xs, (-8.f * (dxA - 8.f)) * rC);  // row 0: sum dx^2 S0
-    PairSums r{w.r0 ? xs : rA, w.r0 ? ys : (w.r2 ? xs : rC), rA};
-    row_halves3_q8(r.X, r.Y, r.Z);
-    return r;
-}
-
 // Per-pixel walk state of one quarter slot k.
 struct PixState { float T, AR; f2v d01; float d2, fy; int lrel; };  // d01: dL/dpix channels 0, 1
 // Running per-lane sums of one walked pair (packed pairs: (S1, S4), (c0, c1)).
-struct LaneSums { float S0; f2v S14, c01; float c2; f2v SB; };  // SB: (S0B, S1B), Q8 only
+struct LaneSums { float S0; f2v S14, c01; float c2; };
 
 // One (pair, quarter) evaluation.  CLAMP: the pair's opacity can exceed 0.99, so alpha may be clamped
 // (wave-uniform, flagged at staging); otherwise alpha = o G exactly and sG = o G T (C - AR) = w (C - AR)
@@ -266,7 +234,7 @@ struct LaneSums { float S0; f2v S14, c01; float c2; f2v SB; };  // SB: (S0B, S1B
 // as the forward did (a tile with more records than kNearCap).  Either way the forward's decisions.
 constexpr int kNearNone = 0, kNearLook = 1, kNearEval = 2;
 struct NearRecs { const float4 *r; uint32_t n; int start; };  // the tile's records, the batch's list start
-template <bool CLAMP, int NEAR, bool Q8>
+template <bool CLAMP, int NEAR>
 __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &any, const PairX &x, float4 a,
                                              float C2, float o, float4 c, int j, int k, float pfx,
                                              const float4 *__restrict__ rec, const uint32_t *__restrict__ pl,
@@ -286,10 +254,7 @@ __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &an
     } else if constexpr (NEAR == kNearLook) {
         const bool nr = live && p2 <= 0.0f && near_threshold(alpha);
         if (nr) {  // (an exec-masked region, skipped when no lane has one)
-            const int l = threadIdx.x & 63;  // the tile pixel 16 y + x of this lane's slot k
-            const uint32_t pix = Q8 ? (uint32_t)(16 * (8 * (k >> 1) + (l >> 3)) + 8 * (k & 1) + (l & 7))
-                                    : (uint32_t)(l + 64 * k);
-            const uint32_t key = ((uint32_t)(nrs.start + j) << 8) | pix;
+            const uint32_t key = ((uint32_t)(nrs.start + j) << 8) | (uint32_t)((threadIdx.x & 63) + 64 * k);
             for (uint32_t i = 0; i < nrs.n; ++i) {  // (uniform loads)
                 const float4 r = nrs.r[i];
                 const bool hit = __float_as_uint(r.x) == key;
@@ -319,13 +284,12 @@ __device__ __forceinline__ void eval_quarter(PixState &ps, LaneSums &s, bool &an
     s.S14 = fma2(f2(gd, u), f2(dy, dy), s.S14);  // S1 += gd dy (fused), S4 += u dy
     s.c01 = fma2(f2(w, w), ps.d01, s.c01);
     s.c2 = fmaf(w, ps.d2, s.c2);
-    if (Q8 && (k & 1)) s.SB = s.SB + f2(gd, u);  // the B column's S0, S1
 }
 
 // The walk of one batch: every staged pair j (descending) over the quarters of its mask; each pair's
 // sums are reduced and added into its s_out slot when any pixel of the wave took it.  CLAMP: some
 // staged pair's opacity exceeds 0.99 (batch-uniform, so the pair loop itself has no variant branch).
-template <bool CLAMP, int NEAR, bool Q8>
+template <bool CLAMP, int NEAR>
 __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const float4 *s_a, float pfx,
                                            const RowW &rw, float *o_row, const float4 *__restrict__ rec,
                                            const uint32_t *__restrict__ pl, const NearRecs &nrs) {
@@ -337,22 +301,18 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
         // wave-uniform quarter mask of the staged entry
         const uint32_t qm = __builtin_amdgcn_readfirstlane(__float_as_uint(c.w));
         const PairX x = pair_x(a, pfx);
-        PairX xb = x;  // Q8: the lane's B column (pfx + 8)
-        if constexpr (Q8) xb = pair_x(a, pfx + 8.f);
         // -0 seeds: x + (-0) == x for every x, so the first contributor needs no add (the ISA folds it)
-        LaneSums s{-0.f, f2(-0.f, -0.f), f2(-0.f, -0.f), -0.f, f2(-0.f, -0.f)};
+        LaneSums s{-0.f, f2(-0.f, -0.f), f2(-0.f, -0.f), -0.f};
         bool any = false;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             if (!(qm & (1u << k))) continue;  // wave-uniform: quarter k cannot reach alpha >= 1/255
-            eval_quarter<CLAMP, NEAR, Q8>(ps[k], s, any, (Q8 && (k & 1)) ? xb : x, a, b.x, b.y, c, j, k,
-                                          (Q8 && (k & 1)) ? pfx + 8.f : pfx, rec, pl, nrs);
+            eval_quarter<CLAMP, NEAR>(ps[k], s, any, x, a, b.x, b.y, c, j, k, pfx, rec, pl, nrs);
         }
         // the skip pays although only ~3 % of the walked pairs have no taker (tools/contrib_stats.py):
         // always reducing measured 0.325 vs 0.316 ms alone (profiles/r05_bwd_micro_ab.txt)
         if (__builtin_amdgcn_ballot_w64(any)) {  // some pixel of the wave took the pair
-            const PairSums sm = Q8 ? pair_sums_q8(s.S0, s.S14.x, s.S14.y, s.SB.x, s.SB.y, s.c01.x, s.c01.y, s.c2, x.dx, rw)
-                                   : pair_sums(s.S0, s.S14.x, s.S14.y, s.c01.x, s.c01.y, s.c2, x.dx, rw);
+            const PairSums sm = pair_sums(s.S0, s.S14.x, s.S14.y, s.c01.x, s.c01.y, s.c2, x.dx, rw);
             if ((threadIdx.x & 14) == 0) {  // lanes 0 and 1 of each row hold its two halves
                 float *o = o_row + j * kPartial;
                 lds_add(o, sm.X);
@@ -367,7 +327,7 @@ __device__ __forceinline__ void walk_batch(PixState (&ps)[4], uint64_t m, const 
 // (x, y, A2, B2); + kStage: (C2, opacity, exact conic a, b); + 2 kStage: colour + quarter mask -- the
 // record's inputs wait in LDS, not in registers, while the batch is walked (but for the exact conic's
 // c and the emission index, which the staging lane keeps).
-template <bool EXACT, bool Q8>
+template <bool EXACT>
 __device__ __forceinline__ void bwd_item(
     uint2 it, uint32_t item, int W, int H, int gx, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
@@ -387,15 +347,12 @@ __device__ __forceinline__ void bwd_item(
     const int n = (int)(rg.y - rg.x);
     const int tx = tile % gx, ty = tile / gx;
     const int lane = threadIdx.x & 63;
-    // pixel k of the lane: 16x4 strips -- column lane & 15, row (lane >> 4) + 4 k; Q8 -- column
-    // 8 (k & 1) + (lane & 7), row 8 (k >> 1) + (lane >> 3) (the forward's 8x8 quarters)
-    const int px = tx * kTileW + (Q8 ? (lane & 7) : (lane & 15));
-    const int py0 = ty * kTileH + (Q8 ? (lane >> 3) : (lane >> 4));
+    const int px = tx * kTileW + (lane & 15);
+    const int py0 = ty * kTileH + (lane >> 4);
     const float pfx = (float)px;
     const float tx0 = (float)(tx * kTileW), ty0 = (float)(ty * kTileH);
     const float tx1 = tx0 + (kTileW - 1);
-    // per quarter-tile maxima of n_contrib (Q8: the 8x8 quarters', stored after the strips')
-    const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[Q8 ? gx * div_up(H, kTileH) + tile : tile];
+    const uint4 mq = reinterpret_cast<const uint4 *>(tile_maxc)[tile];  // per quarter-tile maxima
     const int maxc = min((int)max(max(mq.x, mq.y), max(mq.z, mq.w)), n);
     if (seg & kZeroItem) {  // zero records for one kZeroChunk of the slots past maxc (see bwd_zero_items)
         const int z0 = maxc + (int)kZeroChunk * (int)((seg & ~kZeroItem) + 1);
@@ -426,11 +383,10 @@ __device__ __forceinline__ void bwd_item(
     const size_t bidx = has_bound ? ((size_t)seg_off[tile] + seg) * kTilePix : 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int py = py0 + (Q8 ? 8 * (k >> 1) : 4 * k);
-        const int pxk = px + ((Q8 && (k & 1)) ? 8 : 0);
+        const int py = py0 + 4 * k;
         ps[k].fy = (float)py;
-        const bool inside = pxk < W && py < H;
-        const int pid = py * W + pxk;
+        const bool inside = px < W && py < H;
+        const int pid = py * W + px;
         const float4 pe = inside ? pix_end[pid] : make_float4(0.f, 0.f, 0.f, 0.f);
         // entry p lies before the pixel's last contributor iff p < n_contrib: kept relative to the
         // batch start (lrel = n_contrib - start, advanced per batch)
@@ -440,9 +396,7 @@ __device__ __forceinline__ void bwd_item(
         float bd = 0;
         bd += bg0 * ps[k].d01.x; bd += bg1 * ps[k].d01.y; bd += bg2 * ps[k].d2;
         if (has_bound && qmax[k] >= (uint32_t)s1f) {  // wave-uniform: this quarter resumes at the boundary
-            // the forward's slot of this pixel: 64 (ly >> 2) + 16 (ly & 3) + lx
-            const int lx = pxk - tx * kTileW, ly = py - ty * kTileH;
-            const float4 st = seg_state[bidx + (Q8 ? 64 * (ly >> 2) + 16 * (ly & 3) + lx : 64 * k + lane)];
+            const float4 st = seg_state[bidx + 64 * k + lane];
             ps[k].T = st.w;
             const float behind = ps[k].d01.x * (pe.x - st.x) + ps[k].d01.y * (pe.y - st.y) + ps[k].d2 * (pe.z - st.z);
             ps[k].AR = st.w > 0.f ? (behind + pe.w * bd) / st.w : bd;
@@ -490,12 +444,10 @@ __device__ __forceinline__ void bwd_item(
             s_a[lane] = a;
             s_a[kStage + lane] = make_float4(b.x, b.y, cj.x, cj.y);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float qx0 = Q8 ? tx0 + 8 * (k & 1) : tx0, qy0 = Q8 ? ty0 + 8 * (k >> 1) : ty0 + 4 * k;
-                const float qx1 = Q8 ? qx0 + 7 : tx1, qy1 = qy0 + (Q8 ? 7 : 3);
-                if (p < qmax[k] && !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, qx0, qy0, qx1, qy1))
+            for (int k = 0; k < 4; ++k)
+                if (p < qmax[k] &&
+                    !tile_cull(a.x, a.y, -2.f * a.z, -a.w, -2.f * b.x, b.y, b.w, tx0, ty0 + 4 * k, tx1, ty0 + 4 * k + 3))
                     qmask |= 1u << k;
-            }
             if (qmask && b.y > 0.99f) qmask |= 16u;  // (the batch then takes the clamping walk)
             s_a[2 * kStage + lane] = make_float4(c.x, c.y, c.z, __uint_as_float(qmask));  // .w: the quarter mask
         }
@@ -504,16 +456,16 @@ __device__ __forceinline__ void bwd_item(
         const uint32_t *pl = point_list + rg.x + start;
         const bool clamp = __builtin_amdgcn_ballot_w64(qmask & 16u) != 0;
         if constexpr (EXACT) {
-            if (clamp) walk_batch<true, kNearEval, Q8>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
-            else walk_batch<false, kNearEval, Q8>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+            if (clamp) walk_batch<true, kNearEval>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+            else walk_batch<false, kNearEval>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
         } else {
             nrs.start = start;
             if (nrs.n) {  // (wave-uniform: the tile's forward re-evaluated near-threshold weights)
-                if (clamp) walk_batch<true, kNearLook, Q8>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
-                else walk_batch<false, kNearLook, Q8>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+                if (clamp) walk_batch<true, kNearLook>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+                else walk_batch<false, kNearLook>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
             } else {
-                if (clamp) walk_batch<true, kNearNone, Q8>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
-                else walk_batch<false, kNearNone, Q8>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+                if (clamp) walk_batch<true, kNearNone>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
+                else walk_batch<false, kNearNone>(ps, m, s_a, pfx, rw, o_row, rec, pl, nrs);
             }
         }
         wave_lds_sync();
@@ -543,7 +495,7 @@ __device__ __forceinline__ void bwd_item(
 }
 
 
-template <bool EXACT, bool Q8>
+template <bool EXACT>
 __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     int W, int H, int gx, const uint2 *__restrict__ items, const uint2 *__restrict__ ranges,
     const uint32_t *__restrict__ point_list,
@@ -573,11 +525,11 @@ __global__ __launch_bounds__(64 * kBwdWaves) GSR_BWD_ATTR void k_render_bwd(
     if constexpr (EXACT) {
         // the tiles with more near-threshold weights than kNearCap (rare): every wave loops over them
         for (uint32_t i = blockIdx.x * kBwdWaves + wv; i < hd.y; i += gridDim.x * kBwdWaves)
-            bwd_item<true, Q8>(items[1 + hd.x + i], hd.x + i, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_out);
+            bwd_item<true>(items[1 + hd.x + i], hd.x + i, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_out);
     } else {
         const uint32_t item = blockIdx.x * kBwdWaves + wv;
         if (item >= hd.x) return;  // the launch covers the item bound
-        bwd_item<false, Q8>(items[1 + item], item, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_out);
+        bwd_item<false>(items[1 + item], item, W, H, gx, ranges, point_list, rec, bg, pix_end, n_contrib, tile_maxc, seg_off, seg_state, slot_emit, dL_dpixels, part, ks, tile_flag, near_rec, s_a, s_out);
     }
 }
 
@@ -1411,12 +1363,10 @@ hipError_t launch_render_bwd(const BwdArgs &a, hipStream_t s) {
     // > kNearCap; none when the exact-threshold mode is off) on a small grid that loops over their
     // device-side count.
     const int ks = seg_log2(a.P);
-    auto kf = a.q8 ? k_render_bwd<false, true> : k_render_bwd<false, false>;
-    auto ke = a.q8 ? k_render_bwd<true, true> : k_render_bwd<true, false>;
-    kf<<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(
+    k_render_bwd<false><<<div_up((int)a.max_items, kBwdWaves), 64 * kBwdWaves, 0, s>>>(
         a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg, a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off,
         a.seg_state, a.slot_emit, a.dL_dcolor, a.part, ks, a.spec_ok, a.tile_flag, a.near_rec);
-    ke<<<std::min(div_up((int)a.max_items, kBwdWaves), kExactBwdBlocks), 64 * kBwdWaves, 0, s>>>(
+    k_render_bwd<true><<<std::min(div_up((int)a.max_items, kBwdWaves), kExactBwdBlocks), 64 * kBwdWaves, 0, s>>>(
         a.W, a.H, a.gx, a.items, a.ranges, a.point_list, a.rec, a.bg, a.pix_end, a.n_contrib, a.tile_maxc, a.seg_off,
         a.seg_state, a.slot_emit, a.dL_dcolor, a.part, ks, a.spec_ok, a.tile_flag, a.near_rec);
     return hipGetLastError();

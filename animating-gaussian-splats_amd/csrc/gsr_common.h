@@ -131,6 +131,9 @@ constexpr int kItemsWsWords = 2 * kOrderBuckets + 64;
 // items_ws word counting the pixels the exact saturation re-walk redoes (zeroed with the workspace by
 // k_bin_count; the item kernels use words [0, 2 kOrderBuckets])
 constexpr int kTSatCtr = 2 * kOrderBuckets + 8;
+// records of the pixels the exact saturation re-walk redoes (32 B each, IMAGE tsat_list): one per 8 pixels
+// (measured ~0.1 % of a C3 view's pixels; past the capacity a pixel keeps the fast walk's outputs)
+__host__ __device__ constexpr uint32_t tsat_capacity(int npix) { return (uint32_t)(npix / 8 + 64); }
 
 // The single-pass tile scan of k_bin_colscan (IMAGE.scan_ws, zeroed by k_bin_count): one look-back
 // word per block of tiles (u64: flag in bits 62-63 -- kScanAgg: the block's own sums, kScanInc: the sums
@@ -171,7 +174,7 @@ struct ImageLayout {
         ranges = o;      o = align256(o + sizeof(uint2) * T);
         pix_end = o;     o = align256(o + sizeof(float4) * N);
         n_contrib = o;   o = align256(o + sizeof(uint32_t) * N);
-        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 8 * T);  // per 16x4 strip, then per 8x8 quarter
+        tile_maxc = o;   o = align256(o + sizeof(uint32_t) * 4 * T);  // per quarter tile (16x4 px)
         tile_order_f = o; o = align256(o + sizeof(uint32_t) * T);    // forward dispatch order (LPT)
         seg_off = o;     o = align256(o + sizeof(uint32_t) * (T + 1));
         sort_lists = o;  o = align256(o + sizeof(uint32_t) * T);      // tiles longer than kFwdSortCap
@@ -184,7 +187,7 @@ struct ImageLayout {
         scan_ws = o;     o = align256(o + sizeof(uint32_t) * kScanWsWords);
         tile_rank = o;   o = align256(o + sizeof(uint32_t) * T);           // rank inside its LPT bucket
         tile_flag = o;   o = align256(o + sizeof(uint32_t) * T);           // near-threshold re-evaluations
-        tsat_list = o;   o = align256(o + sizeof(uint32_t) * N);           // pixels the exact re-walk redoes
+        tsat_list = o;   o = align256(o + 32 * (size_t)tsat_capacity(N));  // pixels the exact re-walk redoes
         near_rec = o;    o = align256(o + sizeof(float4) * kNearCap * T);  // and their records
         // (chunk, tile) counts, then each chunk's slab offset inside the tile's range (LDS binning)
         chunk_off = o;   o = align256(o + (T <= kMaxLdsTiles ? sizeof(uint32_t) * (size_t)NB * T : 0));
@@ -629,6 +632,7 @@ __device__ inline bool near_threshold(float alpha) { return alpha >= kNearLo && 
 // every pixel whose final T is below 1e-4 (1 + t_window(n_contrib)) -- the only ones whose stop can
 // differ -- is redone by k_render_tsat, the reference's walk for that pixel with the exact weights.
 constexpr float kTSat = 1e-4f;
+
 constexpr float kTW0 = 5e-5f, kTW1 = 2e-7f;
 __device__ inline float t_window(uint32_t L) { return kTW0 + kTW1 * (float)L; }
 // exact (power, G, alpha) of the Gaussian at (gx, gy) with exact conic (ca, cb, cc) and opacity o.  Not

@@ -866,6 +866,138 @@ __device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *e
     }
 }
 
+// The exact saturation re-walk of one pixel (exact-threshold mode; round 6), by one
+// kTSatThreads-thread block of k_render_tsat (below).  The pixel's final T lies within
+// the drift window of 1e-4 (gsr_common.h t_window), so its stop is recomputed with the reference's
+// transmittance test (SURVEY.md 2.1 row renderCUDA fwd, oracle/gsr_oracle.c ora_render): the threads take
+// kTSatThreads list entries at a time -- the fast weight decides which can contribute, as in the blend (p2 <= 0,
+// alpha >= kNearLo; a weight in the near window is decided by its exact value) -- and each contributor gets
+// its exact weight, min(0.99, o exp(power)) with the reference's expression order and a double-precision
+// exp, and the reference's 1 - alpha (one fp32 rounding), packed in list order into LDS.  Wave 0 then runs
+// the reference's chain test_T = T * (1 - alpha) over them, four multiplies per LDS read (T only
+// decreases: a block of four whose last value is >= 1e-4 keeps all four; the crossing block is stepped
+// through), stopping below 1e-4.  So n_contrib and T are the reference's.  The walk can only end before
+// the fast one (t_stop in the blend), never after it, so only the entries before the fast n_contrib are
+// evaluated.  The fast colour and depth lose the contributions of the entries the fast walk kept past
+// the reference's stop (a few at most, at T ~ 1e-4; their weights from the exact chain continued past
+// the stop).  The pixel's outputs, its end state for the backward and its state at every segment
+// boundary at or past the new n_contrib are written (the earlier boundary states are the fast walk's, as
+// for every other pixel); the tile's quarter maxima stay upper bounds, and every entry the pixel keeps was
+// seen by the fast walk (whose near records the backward looks up).
+constexpr int kTSatThreads = 128;  // threads (list entries per round) of a re-walk block
+struct TSatRec { float4 r0, r1, r3; };  // position + pre-scaled conic, (C2, opacity, ...), exact conic
+__device__ inline TSatRec tsat_load(const float4 *__restrict__ rec, uint32_t g, bool v) {
+    TSatRec t;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 *r = rec + (size_t)kRecF4 * g;
+    t.r0 = v ? r[0] : z; t.r1 = v ? r[1] : z; t.r3 = v ? r[3] : z;
+    return t;
+}
+// entries [0, nf) of the pixel's list, point list [start, start + nf): T, n_contrib and the fast walk's extra
+// contributions E (wave 0's values); the list's point indices two rounds ahead, render records one ahead
+__device__ inline void tsat_chain(int nf, const uint32_t *__restrict__ plist, float pfx, float pfy,
+                                  const float4 *__restrict__ rec, uint32_t *s_rc, float *s_q, float *s_a,
+                                  uint32_t *s_pos, float &T, uint32_t &nex, float4 &E) {
+    constexpr int NT = kTSatThreads, NW = NT / 64;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    float Tc = 0.f;
+    bool stopped = false;
+    uint32_t g_next = t < nf ? plist[t] : 0u;
+    TSatRec cur = tsat_load(rec, g_next, t < nf);
+    g_next = NT + t < nf ? plist[NT + t] : 0u;
+    for (int base = 0; base < nf; base += NT) {
+        const int e = base + t;
+        const TSatRec r = cur;
+        cur = tsat_load(rec, g_next, e + NT < nf);
+        g_next = e + 2 * NT < nf ? plist[e + 2 * NT] : 0u;
+        bool take = false;
+        float al = 0.f;
+        if (e < nf) {
+            const Blend eb = blend_eval<true>(r.r0, r.r1, pfx, pfy);
+            if (eb.p2 <= 0.0f && eb.alpha >= kNearLo) {  // the blend's live test (exact mode)
+                const ExactBlend x = exact_blend(r.r0.x, r.r0.y, r.r3, r.r1.y, pfx, pfy);
+                take = eb.alpha >= kNearHi || (x.power <= 0.0f && x.alpha >= 1.0f / 255.0f);
+                al = x.alpha;
+            }
+        }
+        // pack the contributors in list order: rank = contributors before this thread in the round
+        const uint64_t m = __ballot(take);
+        if (lane == 0) s_rc[wv] = (uint32_t)__builtin_popcountll(m);
+        __syncthreads();
+        uint32_t off = 0, nc = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            off += w < wv ? s_rc[w] : 0u;
+            nc += s_rc[w];
+        }
+        if (take) {
+            const uint32_t rk = off + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            s_q[rk] = 1.0f - al;  // the reference's (1 - alpha), one fp32 rounding
+            s_a[rk] = al;
+            s_pos[rk] = (uint32_t)e;
+        }
+        if (t < 4) s_q[nc + t] = 1.0f;  // padding of the last block of four: T unchanged
+        __syncthreads();
+        if (wv == 0) {  // the reference's chain (wave-uniform values; every lane computes it)
+            const float4 *q4 = reinterpret_cast<const float4 *>(s_q);
+            for (uint32_t k = 0; k < nc; k += 4) {
+                uint32_t j = 0;
+                const uint32_t v = min(4u, nc - k);  // real contributors in the block
+                if (!stopped) {
+                    const float4 q = q4[k >> 2];
+                    const float t1 = T * q.x, t2 = t1 * q.y, t3 = t2 * q.z, t4 = t3 * q.w;
+                    if (t4 >= kTSat) {  // all kept (T only decreases)
+                        T = t4;
+                        nex = s_pos[k + v - 1] + 1u;
+                        continue;
+                    }
+                    // the block crosses: the reference stops at the first value below 1e-4
+                    const float tv[4] = {t1, t2, t3, t4};
+                    while (tv[j] >= kTSat) ++j;  // (j < v: the padding keeps T >= 1e-4)
+                    if (j > 0) {
+                        T = tv[j - 1];
+                        nex = s_pos[k + j - 1] + 1u;
+                    }
+                    stopped = true;
+                    Tc = T;
+                }
+                for (; j < v; ++j) {  // the entries past the stop: the fast walk kept them (rare)
+                    const float a = s_a[k + j];
+                    const float4 c = rec[(size_t)kRecF4 * plist[s_pos[k + j]] + 2];  // (r, g, b, depth)
+                    const float w = a * Tc;
+                    E.x += c.x * w; E.y += c.y * w; E.z += c.z * w; E.w += c.w * w;
+                    Tc = Tc * (1.0f - a);
+                }
+            }
+        }
+        __syncthreads();  // (the round's LDS is reused)
+    }
+}
+// the re-walked pixel's outputs (thread 0) and its segment boundaries at or past the new n_contrib (all)
+__device__ inline void tsat_store(int px, int py, int W, int H, int n, float4 pe, float dfast, float T, uint32_t nex,
+                                  float4 E, const float *__restrict__ bg, float *__restrict__ out_color,
+                                  float *__restrict__ out_depth, float4 *__restrict__ pix_end,
+                                  uint32_t *__restrict__ n_contrib, size_t sb, float4 *__restrict__ seg_state, int ks,
+                                  uint32_t *s_nex) {
+    const int t = threadIdx.x;
+    const int pid = py * W + px;
+    const float4 fin = make_float4(pe.x - E.x, pe.y - E.y, pe.z - E.z, T);
+    if (t == 0) {
+        pix_end[pid] = fin;
+        n_contrib[pid] = nex;
+        out_color[pid] = fin.x + T * bg[0];
+        out_color[H * W + pid] = fin.y + T * bg[1];
+        out_color[2 * H * W + pid] = fin.z + T * bg[2];
+        out_depth[pid] = dfast - E.w;
+    }
+    const uint32_t b0 = (nex + (1u << ks) - 1u) >> ks;  // first boundary index >= n_contrib
+    const int lx = px % kTileW, ly = py % kTileH;
+    const int bslot = 64 * (ly >> 2) + 16 * (ly & 3) + lx;  // the backward's pixel slot
+    const uint32_t nb = n > 0 ? (uint32_t)(n - 1) >> ks : 0u;  // boundaries of the list (1..nb)
+    for (uint32_t q = max(b0, 1u) + (uint32_t)t; q <= nb; q += kTSatThreads)
+        seg_state[(sb + q - 1u) * kTilePix + bslot] = fin;
+    (void)s_nex;
+}
 // 8 waves per SIMD (<= 64 VGPRs): the blend's latency is hidden by occupancy (6 waves: +17 %,
 // profiles/r05_fwd_ilp_ab.txt)
 #define GSR_FWD_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
@@ -879,7 +1011,7 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ spec_ok,
     int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err, uint64_t gate_timeout,
     uint32_t *__restrict__ tile_flag, float4 *__restrict__ near_rec, uint32_t *__restrict__ tsat_n,
-    uint32_t *__restrict__ tsat_list) {
+    uint32_t *__restrict__ tsat_list, uint32_t tsat_cap) {
     __shared__ uint64_t s_key[sort_slots(kFwdSortCap)];
     __shared__ union {
         uint32_t val[sort_slots(kFwdSortCap)];  // sort payload (emission index), until written out
@@ -1051,10 +1183,19 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
         else walk(std::false_type{});
         if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
+    // EXACT: a pixel whose final T lies within the drift window of 1e-4 (gsr_common.h t_window) is redone by
+    // k_render_tsat with the reference's transmittance test; its record carries what that needs
+    // (pixel, list start and length, fast n_contrib, fast colour + depth), so the re-walk starts with one load
+    if (EXACT && inside && Tt < kTSat * (1.0f + t_window(last))) {
+        const uint32_t slot = atomicAdd(tsat_n, 1u);
+        if (slot < tsat_cap) {
+            uint4 *r = reinterpret_cast<uint4 *>(tsat_list) + 2 * (size_t)slot;
+            r[0] = make_uint4((uint32_t)(py * W + px), rg.x, (uint32_t)n, last);
+            r[1] = make_uint4(__float_as_uint(C01.x), __float_as_uint(C01.y), __float_as_uint(C2D.x), __float_as_uint(C2D.y));
+        }
+    }
     if (inside) {
         const int pid = py * W + px;
-        if (EXACT && Tt < kTSat * (1.0f + t_window(last)))  // (rare: k_render_tsat redoes the pixel)
-            tsat_list[atomicAdd(tsat_n, 1u)] = (uint32_t)pid;
         pix_end[pid] = make_float4(C01.x, C01.y, C2D.x, Tt);
         n_contrib[pid] = last;
         out_color[pid] = C01.x + Tt * bg[0];
@@ -1067,9 +1208,6 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     uint32_t mx = last;
 #pragma unroll
     for (int d = 16; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));  // within 32 lanes
-    // and the 8x8 quarter's (this wave's) maximum, after the T strips' (the Q8 backward layout)
-    const uint32_t mq8 = max(mx, (uint32_t)__shfl_xor((int)mx, 32, 64));
-    if (lane == 0) tile_maxc[4 * T + 4 * tile + wv] = mq8;
     __syncthreads();  // every wave is past its last read of s_u
     if (threadIdx.x < 4) s_u.st.q[threadIdx.x] = 0;
     __syncthreads();
@@ -1083,106 +1221,48 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
 #endif
 }
 
-// Exact saturation re-walk (exact-threshold mode; round 6).  One wave per pixel
-// k_render_fwd flagged (final T below 1e-4 (1 + t_window(n_contrib)), gsr_common.h): the reference's
-// front-to-back walk (SURVEY.md 2.1 row renderCUDA fwd, oracle/gsr_oracle.c ora_render) for that one
-// pixel.  The lanes evaluate 64 list entries at a time -- the fast weight decides which can contribute,
-// as in k_render_fwd (p2 <= 0, alpha >= kNearLo; a weight in the near window is decided by its exact
-// value), and every contributor's weight is the exact one, min(0.99, o exp(power)) with the reference's
-// expression order and a double-precision exp -- then the wave applies them in list order with the
-// reference's operations: test_T = T * (1 - alpha), stop below 1e-4, C += c * alpha * T.  So n_contrib,
-// T and the blended colour / depth are the reference's.  The pixel's outputs, its end state for the
-// backward and its state at every segment boundary of the tile's list are rewritten.  The walk can only
-// end earlier than the fast one did (t_stop in k_render_fwd), so only the entries before the fast
-// n_contrib are evaluated, the tile's quarter maxima stay upper bounds, and every entry it takes was
-// seen by the fast walk (whose near records the backward looks up).  Latency-bound by design (a few
-// thousand pixels per 1080p view): the render records of the next 64 entries are in flight while the
-// current ones are applied, and the grid has a wave for every flagged pixel up to kTSatBlocks.
+// The exact saturation re-walk of the pixels k_render_fwd flagged: one 128-thread block per pixel, all in
+// parallel (a fixed grid looping over the device-side count), the walk of tsat_chain / tsat_store above.
+// Each pixel's record (written by k_render_fwd) holds its position, list and fast state, so a block starts
+// with one load.  (A version that re-walked inside k_render_fwd's blocks, after their blend, was slower:
+// the tiles with the most flagged pixels are the long ones at the head of the LPT order)
 constexpr int kTSatBlocks = 4096;
-struct TSatRec { float4 r0, r1, r2, r3; };
-__device__ inline TSatRec tsat_load(const float4 *__restrict__ rec, uint32_t g, bool v) {
-    TSatRec t;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 *r = rec + (size_t)kRecF4 * g;
-    t.r0 = v ? r[0] : z; t.r1 = v ? r[1] : z; t.r2 = v ? r[2] : z; t.r3 = v ? r[3] : z;
-    return t;
-}
-__global__ __launch_bounds__(64) void k_render_tsat(
-    int W, int gx, const uint2 *__restrict__ ranges, const uint32_t *__restrict__ point_list,
-    const float4 *__restrict__ rec, const float *__restrict__ bg, float *__restrict__ out_color,
-    float *__restrict__ out_depth, float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib,
-    const uint32_t *__restrict__ seg_off, float4 *__restrict__ seg_state, const uint32_t *__restrict__ tsat_n,
-    const uint32_t *__restrict__ tsat_list, const uint32_t *__restrict__ spec_ok, int ks, int HW) {
+__global__ __launch_bounds__(kTSatThreads) void k_render_tsat(
+    int W, int H, const uint32_t *__restrict__ point_list, const float4 *__restrict__ rec,
+    const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
+    float4 *__restrict__ pix_end, uint32_t *__restrict__ n_contrib, const uint32_t *__restrict__ seg_off,
+    float4 *__restrict__ seg_state, const uint32_t *__restrict__ tsat_n, const uint32_t *__restrict__ tsat_list,
+    uint32_t tsat_cap, const uint32_t *__restrict__ spec_ok, int ks, int gx) {
+    constexpr int NT = kTSatThreads;
+    __shared__ float4 s_buf[(3 * NT + 4 + 3) / 4];  // the round's contributors: 1 - alpha (+ padding), alpha, position
+    __shared__ uint32_t s_rc[4];   // contributors per wave
     if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
-    const uint32_t cnt = *tsat_n;
-    const int lane = threadIdx.x;
+    const uint32_t cnt = min(*tsat_n, tsat_cap);
+    float *s_q = reinterpret_cast<float *>(s_buf), *s_a = s_q + NT + 4;
+    uint32_t *s_pos = reinterpret_cast<uint32_t *>(s_a + NT);
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-        const uint32_t pid = tsat_list[i];
+        const uint4 *rp = reinterpret_cast<const uint4 *>(tsat_list) + 2 * (size_t)i;
+        const uint4 r0 = rp[0], r1 = rp[1];  // (pixel, list start, length, fast n_contrib), fast (C0, C1, C2, depth)
+        const uint32_t pid = r0.x, start = r0.y;
+        const int n = (int)r0.z, nf = (int)r0.w;
         const int px = (int)(pid % (uint32_t)W), py = (int)(pid / (uint32_t)W);
         const int tile = (py / kTileH) * gx + px / kTileW;
-        const uint2 rg = ranges[tile];
-        const int n = (int)(rg.y - rg.x);
-        const int nf = (int)n_contrib[pid];  // the fast walk's: the exact one ends at or before it
-        const float pfx = (float)px, pfy = (float)py;
-        const int lx = px % kTileW, ly = py % kTileH;
-        const int bslot = 64 * (ly >> 2) + 16 * (ly & 3) + lx;  // the backward's pixel slot (k_render_fwd)
-        const size_t sb = seg_off[tile];
-        float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
-        uint32_t last = 0;
-        bool done = false;
-        // entries base + lane: point list two groups ahead, render records one group ahead
-        uint32_t g_next = lane < nf ? point_list[rg.x + lane] : 0u;
-        TSatRec cur = tsat_load(rec, g_next, lane < nf);
-        g_next = 64 + lane < nf ? point_list[rg.x + 64 + lane] : 0u;
-        for (int base = 0; base < n; base += 64) {
-            // the state in front of entry `base` at a segment boundary (past the stop: the final state)
-            if (base > 0 && (base & ((1 << ks) - 1)) == 0 && lane == 0)
-                seg_state[(sb + ((uint32_t)base >> ks) - 1u) * kTilePix + bslot] = make_float4(C0, C1, C2, T);
-            if (done || base >= nf) continue;
-            const int e = base + lane;
-            const TSatRec t = cur;
-            cur = tsat_load(rec, g_next, e + 64 < nf);
-            g_next = e + 128 < nf ? point_list[rg.x + e + 128] : 0u;
-            bool take = false;
-            float al = 0.f;
-            if (e < nf) {
-                const Blend eb = blend_eval<true>(t.r0, t.r1, pfx, pfy);
-                if (eb.p2 <= 0.0f && eb.alpha >= kNearLo) {  // k_render_fwd's live test (exact mode)
-                    const ExactBlend x = exact_blend(t.r0.x, t.r0.y, t.r3, t.r1.y, pfx, pfy);
-                    take = eb.alpha >= kNearHi || (x.power <= 0.0f && x.alpha >= 1.0f / 255.0f);
-                    al = x.alpha;
-                }
-            }
-            uint64_t m = __ballot(take);
-            while (m) {  // wave-uniform: the reference's serial update, entry by entry
-                const int j = __builtin_ctzll(m);
-                m &= m - 1;
-                const float a = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, al), j));
-                const float test_T = T * (1.0f - a);
-                if (test_T < kTSat) {
-                    done = true;
-                    break;
-                }
-                const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.x), j));
-                const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.y), j));
-                const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.z), j));
-                const float cd = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t.r2.w), j));
-                C0 += cx * a * T;
-                C1 += cy * a * T;
-                C2 += cz * a * T;
-                D += cd * a * T;
-                T = test_T;
-                last = (uint32_t)(base + j + 1);
-            }
+        float T = 1.0f;
+        uint32_t nex = 0;
+        float4 E = make_float4(0.f, 0.f, 0.f, 0.f);
+        tsat_chain(nf, point_list + start, (float)px, (float)py, rec, s_rc, s_q, s_a, s_pos, T, nex, E);
+        if (threadIdx.x == 0) {  // wave 0 holds the result: broadcast through LDS
+            s_rc[0] = nex;
+            s_rc[1] = __float_as_uint(T);
+            s_q[0] = E.x; s_q[1] = E.y; s_q[2] = E.z; s_q[3] = E.w;
         }
-        if (lane == 0) {
-            pix_end[pid] = make_float4(C0, C1, C2, T);
-            n_contrib[pid] = last;
-            out_color[pid] = C0 + T * bg[0];
-            out_color[HW + pid] = C1 + T * bg[1];
-            out_color[2 * HW + pid] = C2 + T * bg[2];
-            out_depth[pid] = D;
-        }
+        __syncthreads();
+        tsat_store(px, py, W, H, n,
+                   make_float4(__uint_as_float(r1.x), __uint_as_float(r1.y), __uint_as_float(r1.z), 0.f),
+                   __uint_as_float(r1.w), __uint_as_float(s_rc[1]), s_rc[0],
+                   make_float4(s_q[0], s_q[1], s_q[2], s_q[3]), bg, out_color, out_depth, pix_end, n_contrib,
+                   seg_off[tile], seg_state, ks, nullptr);
+        __syncthreads();  // (the LDS is reused by the next pixel)
     }
 }
 
@@ -1304,12 +1384,13 @@ hipError_t launch_render_fwd(const FwdArgs &a, hipStream_t s) {
     k<<<T, 256, 0, s>>>(a.W, a.H, a.gx, T, a.tile_order_f, a.ranges, a.pairs,
                         a.point_list, a.slot_emit, a.rec, a.bg, a.out_color, a.out_depth, a.pix_end, a.n_contrib,
                         a.tile_maxc, a.seg_off, a.seg_state, a.spec_ok, seg_log2(a.P), a.gate, a.gate_seq,
-                        a.gate_err, a.gate_timeout, a.tile_flag, a.near_rec, a.items_ws + kTSatCtr, a.tsat_list);
+                        a.gate_err, a.gate_timeout, a.tile_flag, a.near_rec, a.items_ws + kTSatCtr, a.tsat_list,
+                        tsat_capacity(a.W * a.H));
     if (a.exact)  // the flagged pixels' exact re-walk (a fixed grid that loops over the device-side count)
-        k_render_tsat<<<kTSatBlocks, 64, 0, s>>>(a.W, a.gx, a.ranges, a.point_list, a.rec, a.bg, a.out_color,
-                                                 a.out_depth, a.pix_end, a.n_contrib, a.seg_off, a.seg_state,
-                                                 a.items_ws + kTSatCtr, a.tsat_list, a.spec_ok, seg_log2(a.P),
-                                                 a.W * a.H);
+        k_render_tsat<<<kTSatBlocks, kTSatThreads, 0, s>>>(a.W, a.H, a.point_list, a.rec, a.bg, a.out_color, a.out_depth,
+                                                 a.pix_end, a.n_contrib, a.seg_off, a.seg_state, a.items_ws + kTSatCtr,
+                                                 a.tsat_list, tsat_capacity(a.W * a.H), a.spec_ok, seg_log2(a.P),
+                                                 a.gx);
     return hipGetLastError();
 }
 

@@ -47,7 +47,6 @@ constexpr int kSpecSortBlocks = 512;
 
 struct BwdArgs {
     int P, D, M, W, H, gx, gy, K, act;
-    int q8;  // k_render_bwd's 8x8-quarter layout (GSR_BWD_Q8=1; round 6 structural variant)
     float scale_modifier, tan_fovx, tan_fovy, focal_x, focal_y;
     const float *means3D, *scales, *rotations, *shs, *colors_precomp, *cov3D_precomp;
     const float *viewmatrix, *projmatrix, *campos, *bg;

@@ -870,8 +870,8 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer, 
     """Typed views of the arrays inside the forward buffers (for parity tests / debugging);
     ``binning_layout``: the forward's info["binning_layout"] when it enqueued speculatively."""
     L = load_library()
-    offs = (ctypes.c_size_t * 15)()
-    L.gsr_buffer_offsets(int(P), int(W), int(H), int(binning_layout or num_rendered), offs, 15)
+    offs = (ctypes.c_size_t * 16)()
+    L.gsr_buffer_offsets(int(P), int(W), int(H), int(binning_layout or num_rendered), offs, 16)
     o = list(offs)
     T = ((W + 15) // 16) * ((H + 15) // 16)
     K = int(num_rendered)
@@ -899,6 +899,7 @@ def decode_buffers(P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer, 
         "n_contrib": view(imgBuffer, o[7], W * H, i32, (H, W)),
         "tile_maxc": view(imgBuffer, o[8], 4 * T, i32, (T, 4)),
         "tile_flag": view(imgBuffer, o[14], T, i32, (T,)),  # near-threshold re-evaluations (> 16: overflow tile)
+        "tsat_count": view(imgBuffer, o[15], 1, i32, (1,)),  # pixels the exact saturation re-walk redid
         # per-pair records (index, depth bits, emission, 0) in tile-bucket order; keys = .x | .y << 32
         "pairs": view(binningBuffer, o[9], 4 * K, i32, (K, 4)),
         "keys": view(binningBuffer, o[9], 2 * K, i64, (K, 2))[:, 0],

@@ -330,8 +330,9 @@ size_t gsr_spec_binning_bytes(int P, int width, int height, int prepare_backward
  * 128-entry boundary of every tile list: 256 float4 (C0, C1, C2, T) per boundary)}, image
  * {tile_flag (ABI 21: per tile, the count of near-threshold weights the forward re-evaluated inline in
  * the exact-threshold form; their records follow in IMAGE near_rec, at most 16 per tile, and a count
- * above 16 sends the tile's backward items to the re-evaluating k_render_bwd<true>)}.  Returns the count
- * written (15, or max_out if smaller). */
+ * above 16 sends the tile's backward items to the re-evaluating k_render_bwd<true>)}, image {tsat_count
+ * (one word: the pixels the exact saturation re-walk redid, round 6)}.  Returns the count written (16, or
+ * max_out if smaller). */
 int gsr_buffer_offsets(int P, int width, int height, int num_rendered, size_t *out, int max_out);
 
 const char *gsr_last_error(void);

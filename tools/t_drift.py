@@ -33,6 +33,8 @@ for ci in range(min(nviews, len(cams))):
     same = ng == no
     rel = np.abs(tg / np.maximum(to, 1e-30) - 1.0)[same]
     sat = to[same] < 1e-3
+    print(f"{name} view {ci}: re-walked pixels {int(_np(fw['dec']['tsat_count'])[0])}, "
+          f"nf max {int(ng.max())}")
     print(f"{name} view {ci}: pixels {tg.size}, n_contrib differ {int((~same).sum())}, "
           f"max rel T drift {rel.max():.3g} (T<1e-3: {rel[sat].max() if sat.any() else 0:.3g}), "
           f"p99.99 {np.quantile(rel, 0.9999):.3g}; T<1e-3 share {sat.mean():.3f}")
