@@ -28,6 +28,12 @@ namespace gsr {
 
 #ifdef GSR_TRACE
 __device__ uint64_t *g_trace_fwd;
+#ifdef GSR_TRACE
+// the forward waves' work counter: batches << 40 | ticks in the walk << 20 | evaluations
+__device__ inline uint64_t trace_fwd_work(uint64_t batches, uint64_t walk, uint64_t evals) {
+    return (batches << 40) | ((walk < 0xFFFFFull ? walk : 0xFFFFFull) << 20) | (evals < 0xFFFFFull ? evals : 0xFFFFFull);
+}
+#endif
 __device__ uint64_t *g_trace_emit;  // per k_bin_emit block: start, counted, reserved, end
 #define GSR_EMIT_STAMP(k)                                                                        \
     do {                                                                                         \
@@ -1096,6 +1102,9 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
         }                                                                                          \
     } while (0)
     FETCH_BATCH(0);
+#ifdef GSR_TRACE
+    uint64_t tr_batches = 0, tr_walk = 0, tr_entries = 0;  // (diagnostic) batches, walk ticks, evaluations
+#endif
     for (int base = 0; base < n; base += 64) {
         lds_barrier();  // previous batch fully consumed; s_live up to date
         const uint32_t live = s_live;
@@ -1179,8 +1188,16 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
                 take(e, ok, b, c, j);
             }
         };
+#ifdef GSR_TRACE
+        const uint64_t tr_w0 = __builtin_amdgcn_s_memrealtime();
+        tr_batches += 1;
+        tr_entries += (uint64_t)__builtin_popcountll(m);
+#endif
         if (clamp) walk(std::true_type{});
         else walk(std::false_type{});
+#ifdef GSR_TRACE
+        tr_walk += __builtin_amdgcn_s_memrealtime() - tr_w0;
+#endif
         if (((live >> wv) & 1u) && !__ballot(thr < kThrDone) && lane == 0) atomicAnd(&s_live, ~(1u << wv));
     }
     // EXACT: a pixel whose final T lies within the drift window of 1e-4 (gsr_common.h t_window) is redone by
@@ -1217,7 +1234,7 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     // near records of the tile (count; > kNearCap: the backward re-evaluates the tile itself)
     if (threadIdx.x == 0) tile_flag[tile] = EXACT ? s_near : 0u;
 #ifdef GSR_TRACE
-    trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start);
+    trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start, trace_fwd_work(tr_batches, tr_walk, tr_entries));
 #endif
 }
 

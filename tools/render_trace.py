@@ -14,7 +14,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["GSR_LIB"] = os.path.join(REPO, "tools", "libgsr_trace.so")
+os.environ["GSR_LIB"] = os.environ.get("GSR_TRACE_LIB", os.path.join(REPO, "tools", "libgsr_trace.so"))
 sys.path[:0] = [os.path.join(REPO, "animating-gaussian-splats_amd"), REPO]
 
 import numpy as np  # noqa: E402
@@ -84,7 +84,7 @@ def main():
     cams = S.scene_cameras(cfg, device=dev)
     dl = S.upstream_grad(cfg.height, cfg.width, device=dev)
     T = ((cfg.width + 15) // 16) * ((cfg.height + 15) // 16)
-    fbuf = torch.zeros(4 * 4 * T, dtype=torch.int64, device=dev)
+    fbuf = torch.zeros(2 * 4 * 4 * T, dtype=torch.int64, device=dev)  # the view's launch, then k_render_fwd_long
     bbuf = torch.zeros(4 * 16 * T, dtype=torch.int64, device=dev)  # (tile, segment) items
     L.gsr_debug_trace_fwd.argtypes = [ctypes.c_void_p]
     L.gsr_debug_trace_bwd.argtypes = [ctypes.c_void_p]
@@ -105,7 +105,9 @@ def main():
         np.save(os.path.join(REPO, "gpurun_out", f"trace_bwd_cam{ci}.npy"), bbuf.cpu().numpy())
         np.save(os.path.join(REPO, "gpurun_out", f"trace_fwd_cam{ci}.npy"), fbuf.cpu().numpy())
         report[ci] = {"emit": analyse_emit(ebuf.cpu().numpy(), f"cam{ci} emit"),
-                      "fwd": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd"),
+                      "fwd": analyse(fbuf.cpu().numpy(), 8 * T, f"cam{ci} fwd"),
+                      "fwd_view": analyse(fbuf.cpu().numpy(), 4 * T, f"cam{ci} fwd view launch"),
+                      "fwd_long": analyse(fbuf.cpu().numpy()[16 * T:], 4 * T, f"cam{ci} fwd long lists"),
                       "bwd": analyse(bbuf.cpu().numpy(), 16 * T, f"cam{ci} bwd")}
     out = os.path.join(REPO, "gpurun_out")
     os.makedirs(out, exist_ok=True)
