@@ -1165,7 +1165,9 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
             constexpr bool CL = decltype(clamp_c)::value;
             while (m) {
                 const int j = __builtin_ctzll(m);
-                m &= m - 1;
+                // clear bit j: s_lshl_b64 + s_andn2_b64 instead of the 64-bit m - 1 (s_add, s_addc) + s_and
+                // (render_fwd -1.5 % alone, profiles/r06_fwd_bitclr_ab.txt)
+                m &= ~(1ull << j);
                 const float4 a = s_u.st.rec[0][j], b = s_u.st.rec[1][j], c = s_u.st.rec[2][j];
                 Blend e = blend_eval<CL>(a, b, pfx, pfy);
                 bool ok = e.p2 <= 0.0f && e.alpha >= thr;  // blend_ok(e) for a live pixel
