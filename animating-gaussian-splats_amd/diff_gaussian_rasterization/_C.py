@@ -602,11 +602,16 @@ _EXT_STREAMS = {}
 
 
 def _external_stream(ptr, dev):
-    """torch's handle of a library stream (cached per device and stream)."""
+    """torch's handle of a raw stream (cached per device and stream).  Handle 0 is the device's default
+    stream: torch.cuda.ExternalStream(0) is NOT that queue on ROCm -- work put on it ran on a separate
+    hardware queue, unordered with the default stream (round 6: the held-back render halves of deferred
+    views raced the forward and the per-Gaussian pass, tools/spec_half_repro.py, profiles/r06_async_race.txt)."""
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), int(ptr))
     st = _EXT_STREAMS.get(key)
     if st is None:
-        st = _EXT_STREAMS[key] = torch.cuda.ExternalStream(int(ptr), device=torch.device("cuda", key[0]))
+        d = torch.device("cuda", key[0])
+        st = torch.cuda.default_stream(d) if key[1] == 0 else torch.cuda.ExternalStream(key[1], device=d)
+        _EXT_STREAMS[key] = st
     return st
 
 

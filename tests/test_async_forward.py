@@ -274,6 +274,54 @@ def test_speculative_render_half_bitwise(cuda, miss):
         assert torch.equal(ref[1][k], got[1][k]), k
 
 
+@pytest.mark.parametrize("half", [False, True])
+def test_held_back_render_half_on_default_stream(cuda, half):
+    """A deferred view whose asynchronous forward is unresolved at its backward node, on the DEFAULT
+    stream: its render half is queued by the end-of-pass callback (held back, or redone after a missed
+    speculation) on the view's stream, handle 0.  torch.cuda.ExternalStream(0) is a separate queue on
+    ROCm (round 6: those halves raced the forward and the per-Gaussian pass -- NaN or wrong gradients in
+    ~every held-back step, tools/spec_half_repro.py); the view's stream must be the default stream
+    itself.  One view, a denser cloud than the pair-count history, the GPU held busy: bitwise equal to
+    blocking forwards, three times over (the allocator's reuse made the race show from the second)."""
+    P, W, H = 80_000, 480, 320
+    base = S.synthetic_cloud(P, 0.01, seed=7, device=cuda)
+    rs = S.render_settings(W, H, S.intrinsics(400.0, W, H), S.look_at(0, 0.2, 8.0), device=cuda)
+    dl = S.upstream_grad(H, W, device=cuda)
+    with torch.no_grad():
+        act = S.activated_inputs(base, -1)
+
+    def step(scale, busy):
+        leaves = {k: v.detach().clone().requires_grad_(True) for k, v in act.items()}
+        with torch.no_grad():
+            leaves["scales"].mul_(scale)
+        if busy:
+            torch.cuda._sleep(50_000_000)
+        img = GaussianRasterizer(raster_settings=rs)(**dict(leaves, means2D=torch.zeros_like(
+            leaves["means3D"], requires_grad=True)))[0]
+        (img * dl).sum().backward()
+        torch.cuda.synchronize()
+        return img.detach(), {k: v.grad for k, v in leaves.items() if v.grad is not None}
+
+    assert torch.cuda.current_stream().cuda_stream == 0
+    prev_async, prev_half = dgr.set_async_forward(False), dgr._defer["spec_half"]
+    try:
+        dgr._defer["spec_half"] = half
+        ref = step(3.0, False)
+        for _ in range(3):
+            dgr.set_async_forward(False)
+            _C.speculation_stats(reset=True)
+            step(1.0, False)  # pair-count history of the sparse cloud: the capacity stands, K unknown
+            dgr.set_async_forward(True)
+            got = step(3.0, True)
+            assert torch.equal(ref[0], got[0])
+            assert ref[1].keys() == got[1].keys()
+            for k in ref[1]:
+                assert torch.equal(ref[1][k], got[1][k]), k
+    finally:
+        dgr.set_async_forward(prev_async)
+        dgr._defer["spec_half"] = prev_half
+
+
 @pytest.mark.parametrize("shape", ["call", "autograd"])
 def test_gate_timeout_fails_that_steps_backward(cuda, shape):
     """A failed speculation whose redo the resolver holds back longer than the gate's timeout (test hook

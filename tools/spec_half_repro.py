@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--stash", action="store_true",
                     help="keep every render half's SUMS (no synchronisation) and compare them after the step")
     ap.add_argument("--nofresh", action="store_true", help="zero-filled gradient targets (_defer['fresh'] off)")
+    ap.add_argument("--views-twice", action="store_true",
+                    help="after the per-Gaussian pass, synchronise and run it again into zeroed targets, compare")
     ap.add_argument("--hold", default="", help="keep extra references: 'fwd' (every _C._forward result), "
                     "'half' (every render half's return), 'both'")
     ap.add_argument("--probe", action="store_true",
@@ -69,6 +71,22 @@ def main():
     print(f"visible in some view: {int(vis.sum())} of {P}", flush=True)
     if args.nofresh:
         dgr._defer["fresh"] = False
+    if args.views_twice:
+        orig_views = _C.rasterize_gaussians_backward_views
+
+        def views_twice(views, *a, accumulate_into=None, overwrite=(), needed=None, **k):
+            r = orig_views(views, *a, accumulate_into=accumulate_into, overwrite=overwrite, needed=needed, **k)
+            torch.cuda.synchronize()
+            first = [None if t is None else t.clone() for t in accumulate_into]
+            fresh = [None if t is None else torch.zeros_like(t) for t in accumulate_into]
+            vs = [dict(v, means2D_grad=None) for v in views]
+            orig_views(vs, *a, accumulate_into=fresh, overwrite=(), needed=needed, **k)
+            torch.cuda.synchronize()
+            d = [None if f is None else float((f - g).abs().nan_to_num(1e30).max()) for f, g in zip(first, fresh)]
+            print(f"  views pass: {len(views)} views, K {[v['num_rendered'] for v in views]}; again after a sync "
+                  f"into zeroed targets, max diff per slot {d}", flush=True)
+            return r
+        _C.rasterize_gaussians_backward_views = views_twice
 
     def cmp(label, ref, got):
         im = all(torch.equal(x, y) for x, y in zip(ref[0], got[0]))
