@@ -274,6 +274,15 @@ def test_speculative_render_half_bitwise(cuda, miss):
         assert torch.equal(ref[1][k], got[1][k]), k
 
 
+def test_external_stream_of_handle_zero_is_the_default_stream(cuda):
+    """The deferred backward's stream lookup: raw handle 0 must give torch's default stream (the same
+    queue as the forward), a real handle the stream it names (round 6)."""
+    assert _C._external_stream(0, cuda) == torch.cuda.default_stream(cuda)
+    s = torch.cuda.Stream(device=cuda)
+    e = _C._external_stream(s.cuda_stream, cuda)
+    assert e.cuda_stream == s.cuda_stream
+
+
 @pytest.mark.parametrize("half", [False, True])
 def test_held_back_render_half_on_default_stream(cuda, half):
     """A deferred view whose asynchronous forward is unresolved at its backward node, on the DEFAULT
