@@ -890,7 +890,10 @@ __device__ inline void gate_wait(const uint32_t *gate, uint32_t seq, uint32_t *e
 // boundary at or past the new n_contrib are written (the earlier boundary states are the fast walk's, as
 // for every other pixel); the tile's quarter maxima stay upper bounds, and every entry the pixel keeps was
 // seen by the fast walk (whose near records the backward looks up).
-constexpr int kTSatThreads = 128;  // threads (list entries per round) of a re-walk block
+#ifndef GSR_TSAT_THREADS  // 64: render_fwd alone -1.2 % against 128 (and 256), profiles/r06_tsat_threads_ab.txt
+#define GSR_TSAT_THREADS 64
+#endif
+constexpr int kTSatThreads = GSR_TSAT_THREADS;  // threads (list entries per round) of a re-walk block
 struct TSatRec { float4 r0, r1, r3; };  // position + pre-scaled conic, (C2, opacity, ...), exact conic
 __device__ inline TSatRec tsat_load(const float4 *__restrict__ rec, uint32_t g, bool v) {
     TSatRec t;
@@ -1240,7 +1243,7 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
 #endif
 }
 
-// The exact saturation re-walk of the pixels k_render_fwd flagged: one 128-thread block per pixel, all in
+// The exact saturation re-walk of the pixels k_render_fwd flagged: one kTSatThreads-thread block per pixel, all in
 // parallel (a fixed grid looping over the device-side count), the walk of tsat_chain / tsat_store above.
 // Each pixel's record (written by k_render_fwd) holds its position, list and fast state, so a block starts
 // with one load.  (A version that re-walked inside k_render_fwd's blocks, after their blend, was slower:
