@@ -8,6 +8,8 @@
   over the views of the oracle's per-view backward, and every view's image with the oracle's.  Run
   twice: one ``means2D`` leaf shared by the 5 views (the bench) and one fresh ``means2D`` leaf per
   view (create_render_arguments makes one per render, shared.py:38-41).
+* C3M (bench.py --config C3M, round 6): one view of the clustered 1M cloud (lists up to ~21k pairs),
+  image and every gradient against the oracle with no allowance.
 * C5 (BASELINE.json configs[4]): one view of the 2M-Gaussian RGB cloud at 1920x1080 through
   ``rasterize_parameters`` (the C5 fit's fused activations) against the oracle on torch's CPU
   activations, chained back to the raw parameters by CPU autograd.
@@ -133,3 +135,38 @@ def test_c5_view_vs_oracle(cuda):
     for k in ("opacity_logits", "log_scales", "rotation_quaternions"):
         _close(f"C5 {k}", _np(gp[k].grad), raw[k].grad.numpy(), max_bad_frac=allow["grad"])
     STATS.append(("test_c5_view_vs_oracle", "num_rendered", float(st["num_rendered"]), 0.0, 0.0))
+
+
+def test_c3m_view_vs_oracle(cuda):
+    """One view of the clustered C3M cloud (bench.py --config C3M: half of the 1M means in 16 tight blobs,
+    SH3, 1920x1080): tile lists up to ~21k pairs take every sort path (merge sort included) and the long
+    walks' segment states; image, n_contrib and every gradient against the oracle, no allowance."""
+    cfg = S.CONFIGS["C3"]
+    p = S.clustered_cloud(cfg.P, cfg.s0, sh_degree=3, seed=0, device="cpu")
+    a = {k: v.detach() for k, v in S.activated_inputs(p, 3).items() if isinstance(v, torch.Tensor)}
+    a.pop("means2D")
+    rs = S.render_settings(cfg.width, cfg.height, S.intrinsics(cfg.focal, cfg.width, cfg.height),
+                           S.look_at(*S.RIG27[0], cfg.distance), device="cpu", sh_degree=3)
+    st = O.forward(rs.bg.numpy(), a["means3D"].numpy(), None, a["opacities"].numpy(), a["scales"].numpy(),
+                   a["rotations"].numpy(), 1.0, None, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy,
+                   rs.image_height, rs.image_width, a["shs"].numpy(), 3, rs.campos.numpy())
+    assert int(np.diff(st["ranges"].astype(np.int64), axis=1).max()) > 16384  # merge-sorted lists
+    dl = S.upstream_grad(cfg.height, cfg.width, device="cpu")
+    g = O.backward(st, dl.numpy())
+    leaves = {k: v.to(cuda).requires_grad_(True) for k, v in a.items()}
+    m2 = torch.zeros(cfg.P, 3, device=cuda, requires_grad=True)
+    rsg = rs._replace(bg=rs.bg.to(cuda), viewmatrix=rs.viewmatrix.to(cuda), projmatrix=rs.projmatrix.to(cuda),
+                      campos=rs.campos.to(cuda))
+    from diff_gaussian_rasterization import GaussianRasterizer
+    color, radii, depth = GaussianRasterizer(raster_settings=rsg)(
+        means3D=leaves["means3D"], means2D=m2, shs=leaves["shs"], opacities=leaves["opacities"],
+        scales=leaves["scales"], rotations=leaves["rotations"])
+    (color * dl.to(cuda)).sum().backward()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_np(radii), st["radii"])
+    _close("C3M color", _np(color), st["color"], atol_frac=1e-6)
+    _close("C3M depth", _np(depth), st["depth"], atol_frac=1e-6)
+    _close("C3M means2D", _np(m2.grad), g["means2D"])
+    for leaf, ref in (("means3D", "means3D"), ("opacities", "opacities"), ("scales", "scales"),
+                      ("rotations", "rotations"), ("shs", "sh")):
+        _close(f"C3M {leaf}", _np(leaves[leaf].grad), g[ref])
