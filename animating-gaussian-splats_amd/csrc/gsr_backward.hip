@@ -1079,32 +1079,9 @@ __global__ __launch_bounds__(256) void k_sum_records(int P, const uint32_t *__re
 // Against one k_gauss_bwd per view this removes (V - 1) reads of the parameters and (V - 1)
 // read-modify-writes of every gradient array: at SH3 ~ 0.6 KB of HBM traffic per Gaussian per view.
 // Per view the screen-space gradient goes to that view's own dL/dmeans2D array.
-// Round 6, GSR_MV_SPLIT: at SH3 only coefficients 0-8 are staged in LDS (27 floats
-// per thread instead of 49), coefficients 9-15 are read from global memory by each view's direction
-// gradient (L2 hits after the first view), dL/dSH is summed in registers and stored per thread, and the
-// kernel is held to 4 waves/SIMD (<= 128 VGPRs): 3 waves were held by LDS and VGPRs at once.
-#ifndef GSR_MV_SPLIT
-#define GSR_MV_SPLIT 0
-#endif
-#if GSR_MV_SPLIT
-#define GSR_MV_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-#else
 #define GSR_MV_ATTR  // (the compiler's register budget: 4 waves/SIMD spilled)
-#endif
-constexpr int kMvLdsCoeffs = 9;  // (GSR_MV_SPLIT) coefficients per row staged in LDS at SH3
 template <int MC>
-constexpr bool mv_split() { return GSR_MV_SPLIT && MC == 16; }
-template <int MC>
-constexpr int mv_row_len() { return mv_split<MC>() ? 3 * kMvLdsCoeffs : 3 * MC; }  // floats per LDS row
-template <int MC>
-constexpr int mv_row_stride() { return mv_split<MC>() ? 3 * kMvLdsCoeffs : sh_row_stride(MC); }  // (27: odd)
-// (GSR_MV_SPLIT) a coefficient row: the first kMvLdsCoeffs coefficients from LDS, the rest from global
-struct ShRowSplit {
-    const float *lds, *glb;
-    __device__ float operator[](int k) const { return k < 3 * kMvLdsCoeffs ? lds[k] : glb[k]; }
-};
-template <int MC>
-constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * mv_row_stride<MC>() + 3) & ~size_t(3)) : 0; }
+constexpr size_t multi_sh_floats() { return MC ? (((size_t)kShBlock * sh_row_stride(MC) + 3) & ~size_t(3)) : 0; }
 template <int MC>
 constexpr size_t multi_lds_bytes() { return sizeof(float) * multi_sh_floats<MC>(); }
 
@@ -1140,7 +1117,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
     const int i = i0 + threadIdx.x;
     const bool live = i < P;
     const int ii = live ? i : i0;  // lanes past P load (and never store) row i0's parameters
-    float *s_row = s_sh + threadIdx.x * (mv_split<MC>() ? mv_row_stride<MC>() : RS);
+    float *s_row = s_sh + threadIdx.x * RS;
     const uint32_t ord = view_order(a);
     auto vid = [ord](int t) { return (int)((ord >> (4 * t)) & 15u); };  // the view summed t-th
     // the Gaussian's own parameters and the first view's record sums and radius are loaded before the
@@ -1163,10 +1140,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
 #pragma unroll
     for (int k = 0; k < kPartial; ++k) nx[k] = a.v[vid(0)].sums[(size_t)k * P + ii];
     int rn = a.v[vid(0)].radii[ii];
-    if constexpr (mv_split<MC>()) {  // coefficients 0-8 of each row (the rest: global, per view)
-        sh_rows_to_lds_cols<RL, mv_row_len<MC>(), mv_row_stride<MC>()>(a.shs + (size_t)i0 * RL, nrow, s_sh);
-        __syncthreads();
-    } else if constexpr (MC > 0) {  // coefficient rows, read by every view's SH chain
+    if constexpr (MC > 0) {  // coefficient rows, read by every view's SH chain
         sh_rows_to_lds<MC>(a.shs + (size_t)i0 * RL, nrow, s_sh);
         __syncthreads();
     }
@@ -1244,10 +1218,7 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
             const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
             const float dRGB[3] = {acc[6] * (cl[0] ? 0.f : 1.f), acc[7] * (cl[1] ? 0.f : 1.f),
                                    acc[8] * (cl[2] ? 0.f : 1.f)};
-            float3 dd;
-            if constexpr (mv_split<MC>()) dd = sh_dir_grad(a.D, x, y, z, ShRowSplit{s_row, a.shs + (size_t)ii * RL}, dRGB);
-            else dd = sh_dir_grad(a.D, x, y, z, s_row, dRGB);
-            const float3 d = unit_vec_bwd(d0, dd);
+            const float3 d = unit_vec_bwd(d0, sh_dir_grad(a.D, x, y, z, s_row, dRGB));
             dm0 += d.x; dm1 += d.y; dm2 += d.z;
         }
         gm0 += dm0; gm1 += dm1; gm2 += dm2;
@@ -1325,44 +1296,6 @@ __global__ __launch_bounds__(kShBlock) GSR_MV_ATTR void k_gauss_bwd_multi(const 
         // additions in the same order as running sums over the views.  dRGB_v is reloaded from the
         // view's sums, the clamp mask and direction recomputed as in the loop.
         if (!a.dL_dsh) return;
-        if constexpr (mv_split<MC>()) {  // the sums in registers, each thread stores its own row
-            if (!live) return;
-            float acc_sh[RL];
-#pragma unroll
-            for (int k = 0; k < RL; ++k) acc_sh[k] = 0.f;
-            for (int t = 0; t < a.nv; ++t) {
-                const MultiView &V = a.v[vid(t)];
-                if (!(V.radii[i] > 0)) continue;
-                const float3 cp = load_campos(V.campos, V.cs.c0);
-                bool cl[3];
-                clamp_from_mask(V.clampm[i], cl);
-                const float g[3] = {V.sums[(size_t)6 * P + i], V.sums[(size_t)7 * P + i], V.sums[(size_t)8 * P + i]};
-                const float3 d0 = make_float3(mean.x - cp.x, mean.y - cp.y, mean.z - cp.z);
-                const float len = sqrtf(d0.x * d0.x + d0.y * d0.y + d0.z * d0.z);
-                const float x = d0.x / len, y = d0.y / len, z = d0.z / len;
-                const float dRGB[3] = {g[0] * (cl[0] ? 0.f : 1.f), g[1] * (cl[1] ? 0.f : 1.f), g[2] * (cl[2] ? 0.f : 1.f)};
-                float basis[16];
-                sh_basis16(x, y, z, basis);
-#pragma unroll
-                for (int k = 0; k < MC; ++k)
-                    if (k < active) {
-#pragma unroll
-                        for (int c = 0; c < 3; ++c) acc_sh[3 * k + c] += basis[k] * dRGB[c];
-                    }
-            }
-            float4 *d4 = reinterpret_cast<float4 *>(a.dL_dsh + (size_t)i * RL);  // (192-byte rows)
-            const bool acc = a.accm & GSR_GRAD_SH;
-#pragma unroll
-            for (int q = 0; q < RL / 4; ++q) {
-                float4 v = make_float4(acc_sh[4 * q], acc_sh[4 * q + 1], acc_sh[4 * q + 2], acc_sh[4 * q + 3]);
-                if (acc) {
-                    const float4 o = d4[q];
-                    v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
-                }
-                d4[q] = v;
-            }
-            return;
-        }
         if (live) {
 #pragma unroll
             for (int k = 0; k < RL; ++k) s_row[k] = 0.f;

@@ -290,45 +290,6 @@ __device__ inline void sh_rows_to_lds(const float *__restrict__ src, int nrow, f
     }
 }
 
-// The same copy restricted to the first NC floats of each RL-float row, into LDS rows of stride RS
-// (k_gauss_bwd_multi with GSR_MV_SPLIT).  Whole rows are read (float4, coalesced), the rest discarded.
-template <int RL, int NC, int RS>
-__device__ inline void sh_rows_to_lds_cols(const float *__restrict__ src, int nrow, float *s) {
-    constexpr int IT = (kShBlock * RL / 4 + kShBlock - 1) / kShBlock;
-    const int n = nrow * RL;
-    if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-        const int n4 = n >> 2;
-        const float4 *s4 = reinterpret_cast<const float4 *>(src);
-        float4 v[IT];
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int q = threadIdx.x + it * kShBlock;
-            if (q < n4) v[it] = s4[q];
-        }
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int q = threadIdx.x + it * kShBlock;
-            if (q < n4) {
-                const float f[4] = {v[it].x, v[it].y, v[it].z, v[it].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = 4 * q + j, r = e / RL, c = e - r * RL;
-                    if (c < NC) s[r * RS + c] = f[j];
-                }
-            }
-        }
-        for (int e = 4 * n4 + (int)threadIdx.x; e < n; e += kShBlock) {
-            const int r = e / RL, c = e - r * RL;
-            if (c < NC) s[r * RS + c] = src[e];
-        }
-    } else {
-        for (int e = threadIdx.x; e < n; e += kShBlock) {
-            const int r = e / RL, c = e - r * RL;
-            if (c < NC) s[r * RS + c] = src[e];
-        }
-    }
-}
-
 // The reverse copy (LDS rows -> contiguous global rows), float4 stores when aligned; ACC adds the
 // rows to what dst holds (gradient accumulation).
 template <int MC, bool ACC = false>
