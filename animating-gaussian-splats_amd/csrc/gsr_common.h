@@ -20,7 +20,10 @@ constexpr int kPartial = 9;  // per (tile, Gaussian) backward partial: dmean2D x
 constexpr int kRecF = kPartial;  // floats per stored partial-gradient record (36 bytes, packed)
 constexpr int kSortCap = 4096;  // per-tile list length sorted entirely in LDS (32 KiB of u64 keys)
 __host__ __device__ inline uint64_t pair_key(uint4 r) { return ((uint64_t)r.y << 32) | r.x; }
-constexpr int kFwdSortCap = 1024;  // lists up to this length are depth-sorted inside k_render_fwd
+#ifndef GSR_FWD_SORT_CAP
+#define GSR_FWD_SORT_CAP 1024
+#endif
+constexpr int kFwdSortCap = GSR_FWD_SORT_CAP;  // lists up to this length are depth-sorted inside k_render_fwd
 // host-mapped words published by k_bin_scan: [0] = K (written last, release), [1] = number of
 // tiles with kFwdSortCap < n <= kSortCap pairs (k_tile_sort), [2] = number of longer tiles (chunk
 // sort + merge passes), [3] = the longest list

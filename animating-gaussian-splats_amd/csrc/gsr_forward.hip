@@ -1021,9 +1021,9 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     int ks, const uint32_t *gate, uint32_t gate_seq, uint32_t *gate_err, uint64_t gate_timeout,
     uint32_t *__restrict__ tile_flag, float4 *__restrict__ near_rec, uint32_t *__restrict__ tsat_n,
     uint32_t *__restrict__ tsat_list, uint32_t tsat_cap) {
-    __shared__ uint64_t s_key[sort_slots(kFwdSortCap)];
+    __shared__ uint64_t s_key[sort_slots(kFwdSortCap > 0 ? kFwdSortCap : 1)];
     __shared__ union {
-        uint32_t val[sort_slots(kFwdSortCap)];  // sort payload (emission index), until written out
+        uint32_t val[sort_slots(kFwdSortCap > 0 ? kFwdSortCap : 1)];  // sort payload (emission index), until written out
         struct {
             // then: the staged batch of 64 render records, part q of entry e at rec[q][e]; rows padded by
             // 2 float4 so that the staging stores of one entry's 3 parts (lanes 4e + q) fall in distinct
@@ -1084,6 +1084,9 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     const uint32_t pix_key = (uint32_t)(16 * ly + lx);  // near record key: (list position << 8) | pixel
     if (threadIdx.x == 0) s_live = 0;
     __syncthreads();  // sort outputs consumed / s_live cleared
+#ifdef GSR_TRACE
+    const uint64_t tr_sorted = __builtin_amdgcn_s_memrealtime();  // (diagnostic) the in-render sort's end
+#endif
     if (__ballot(thr < kThrDone) && lane == 0) atomicOr(&s_live, 1u << wv);
     float Tt = 1.0f;
     f2v C01 = f2(0.f, 0.f), C2D = f2(0.f, 0.f);  // (C0, C1), (C2, depth): packed accumulators
@@ -1240,6 +1243,8 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
     if (threadIdx.x == 0) tile_flag[tile] = EXACT ? s_near : 0u;
 #ifdef GSR_TRACE
     trace_wave(g_trace_fwd, 4 * blockIdx.x + wv, t_start, trace_fwd_work(tr_batches, tr_walk, tr_entries));
+    if (g_trace_fwd && lane == 0)  // ticks to the sort's end, above the HW_ID / XCC_ID word's 40 bits
+        g_trace_fwd[4 * (4 * blockIdx.x + wv) + 2] |= (tr_sorted - t_start) << 40;
 #endif
 }
 
