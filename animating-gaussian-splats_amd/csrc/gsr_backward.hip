@@ -171,7 +171,10 @@ __device__ inline void rec_store(float4 *part, uint32_t em, float r0, float r1, 
 // The near-overflow variant keeps 4 (its re-evaluation call site needs the registers).
 #define GSR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(EXACT ? 4 : 7, 8)))
 constexpr int kBwdWaves = 4;  // items (one wave each) per workgroup
-constexpr int kExactBwdBlocks = 256;  // grid of the exact-threshold tiles' k_render_bwd
+#ifndef GSR_EXACT_BWD_BLOCKS
+#define GSR_EXACT_BWD_BLOCKS 256
+#endif
+constexpr int kExactBwdBlocks = GSR_EXACT_BWD_BLOCKS;  // grid of the exact-threshold tiles' k_render_bwd
 
 // ---- the pair reduction ---------------------------------------------------------------------------
 // Every lane holds, for its 4 pixels of one column, S0 = sum sG, S1 = sum sG dy, S4 = sum sG dy^2 and

@@ -1253,7 +1253,10 @@ __global__ __launch_bounds__(256) GSR_FWD_ATTR void k_render_fwd(
 // Each pixel's record (written by k_render_fwd) holds its position, list and fast state, so a block starts
 // with one load.  (A version that re-walked inside k_render_fwd's blocks, after their blend, was slower:
 // the tiles with the most flagged pixels are the long ones at the head of the LPT order)
-constexpr int kTSatBlocks = 4096;
+#ifndef GSR_TSAT_BLOCKS
+#define GSR_TSAT_BLOCKS 4096
+#endif
+constexpr int kTSatBlocks = GSR_TSAT_BLOCKS;
 __global__ __launch_bounds__(kTSatThreads) void k_render_tsat(
     int W, int H, const uint32_t *__restrict__ point_list, const float4 *__restrict__ rec,
     const float *__restrict__ bg, float *__restrict__ out_color, float *__restrict__ out_depth,
