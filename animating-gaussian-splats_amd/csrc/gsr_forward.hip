@@ -1268,9 +1268,15 @@ __global__ __launch_bounds__(kTSatThreads) void k_render_tsat(
     __shared__ uint32_t s_rc[4];   // contributors per wave
     if (spec_ok && *spec_ok == 0u) return;  // speculative launch whose capacity failed: redone by the host
     const uint32_t cnt = min(*tsat_n, tsat_cap);
+#ifdef GSR_TRACE
+    const uint64_t tr_b = __builtin_amdgcn_s_memrealtime();  // (diagnostic) the block's start
+#endif
     float *s_q = reinterpret_cast<float *>(s_buf), *s_a = s_q + NT + 4;
     uint32_t *s_pos = reinterpret_cast<uint32_t *>(s_a + NT);
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+#ifdef GSR_TRACE
+        const uint64_t tr_i = __builtin_amdgcn_s_memrealtime();
+#endif
         const uint4 *rp = reinterpret_cast<const uint4 *>(tsat_list) + 2 * (size_t)i;
         const uint4 r0 = rp[0], r1 = rp[1];  // (pixel, list start, length, fast n_contrib), fast (C0, C1, C2, depth)
         const uint32_t pid = r0.x, start = r0.y;
@@ -1281,6 +1287,9 @@ __global__ __launch_bounds__(kTSatThreads) void k_render_tsat(
         uint32_t nex = 0;
         float4 E = make_float4(0.f, 0.f, 0.f, 0.f);
         tsat_chain(nf, point_list + start, (float)px, (float)py, rec, s_rc, s_q, s_a, s_pos, T, nex, E);
+#ifdef GSR_TRACE
+        const uint64_t tr_c = __builtin_amdgcn_s_memrealtime();
+#endif
         if (threadIdx.x == 0) {  // wave 0 holds the result: broadcast through LDS
             s_rc[0] = nex;
             s_rc[1] = __float_as_uint(T);
@@ -1293,6 +1302,18 @@ __global__ __launch_bounds__(kTSatThreads) void k_render_tsat(
                    make_float4(s_q[0], s_q[1], s_q[2], s_q[3]), bg, out_color, out_depth, pix_end, n_contrib,
                    seg_off[tile], seg_state, ks, nullptr);
         __syncthreads();  // (the LDS is reused by the next pixel)
+#ifdef GSR_TRACE
+        // (diagnostic, tools/tsat_trace.py) per pixel after the forward's 4T wave slots: (start, end,
+        // fast n_contrib | list length << 32, chain ticks | ticks since the block's start << 32)
+        const uint32_t ntile = (uint32_t)gx * (uint32_t)((H + kTileH - 1) / kTileH);
+        if (g_trace_fwd && threadIdx.x == 0 && i < 4u * ntile) {
+            uint64_t *o = g_trace_fwd + 16 * (size_t)ntile + 4 * (size_t)i;
+            o[0] = tr_i;
+            o[1] = __builtin_amdgcn_s_memrealtime();
+            o[2] = (uint64_t)(uint32_t)nf | ((uint64_t)(uint32_t)n << 32);
+            o[3] = (tr_c - tr_i) | ((tr_i - tr_b) << 32);
+        }
+#endif
     }
 }
 
